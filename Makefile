@@ -1,0 +1,54 @@
+# Build of the MI355X-native heat engine.
+#   make            -> parallel_heat_amd/_lib/libheat.so  and  build/heat (CLI)
+#   make asm        -> gfx950 ISA of the kernels in build/asm/ (inspection)
+#   make resources  -> per-kernel VGPR/SGPR/LDS/occupancy report
+# Everything targets gfx950 only (MI355X / CDNA4).
+ROCM    ?= /opt/rocm
+HIPCC   ?= $(ROCM)/bin/hipcc
+ARCH    ?= gfx950
+BUILD   ?= build
+LIBDIR  := parallel_heat_amd/_lib
+CXXSTD  := -std=c++17
+# Host code: x86-64-v3 (FMA/AVX2) so the CPU oracle's fmaf is a single
+# instruction; device code: gfx950.
+COMMON  := $(CXXSTD) -O3 -fPIC -Wall -Wno-unused-result -Icsrc/include -mfma -mavx2 \
+           -fopenmp -D__HIP_PLATFORM_AMD__
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+LDFLAGS := -fopenmp -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+SRCS_CPP := $(wildcard csrc/src/*.cpp)
+SRCS_HIP := $(wildcard csrc/kernels/*.hip)
+HDRS     := $(wildcard csrc/include/heat/*.hpp csrc/include/heat/*.h)
+OBJS     := $(patsubst csrc/src/%.cpp,$(BUILD)/obj/%.o,$(SRCS_CPP)) \
+            $(patsubst csrc/kernels/%.hip,$(BUILD)/obj/%.o,$(SRCS_HIP))
+
+all: $(LIBDIR)/libheat.so $(BUILD)/heat
+
+$(BUILD)/obj/%.o: csrc/src/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(BUILD)/obj/%.o: csrc/kernels/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libheat.so: $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) $(LDFLAGS)
+
+$(BUILD)/heat: csrc/apps/heat_main.cpp $(OBJS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -x hip csrc/apps/heat_main.cpp -x none $(OBJS) -o $@ $(LDFLAGS)
+
+asm: $(SRCS_HIP)
+	@mkdir -p $(BUILD)/asm
+	cd $(BUILD)/asm && for f in $(SRCS_HIP); do \
+	  $(HIPCC) $(patsubst -Icsrc/include,-I../../csrc/include,$(HIPFLAGS)) --offload-device-only -S -o $$(basename $$f .hip).s ../../$$f; done
+
+resources: $(SRCS_HIP)
+	$(HIPCC) $(HIPFLAGS) -c csrc/kernels/stencil.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \
+	  grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|LDS Size" | paste - - - - - - -
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)/libheat.so
+
+.PHONY: all asm resources clean

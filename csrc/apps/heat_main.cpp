@@ -1,0 +1,304 @@
+// `heat` — the standalone command-line entry point.
+//
+// One binary replaces the reference's compile-time variants
+// (cuda_heat, heat_<N>, heat_omp_<N>, heat_con_<N>, heat_con_omp_<N>;
+// cuda/Makefile:13-17, mpi/Makefile:12-22): every -D macro is a flag here.
+// Multi-process runs read RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR (any
+// launcher, e.g. `python -m torch.distributed.run`), use TCP between CPU
+// ranks and RCCL between GPU ranks (the RCCL unique id travels over the TCP
+// rendezvous).  Output lines reproduce the reference's (mpi/...c:88-96,
+// :298-306; cuda/cuda_heat.cu:254-260) under --naming mpi|cuda.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "heat/capi.h"
+#include "heat/common.hpp"
+#include "heat/io.hpp"
+#include "heat/solver.hpp"
+
+using namespace heat;
+
+namespace {
+
+void usage() {
+  std::printf(
+      "usage: heat [options]\n"
+      "  --nx N --ny N           grid size (rows x columns)            [20 x 20]\n"
+      "  --steps N               time steps                             [10000]\n"
+      "  --cx F --cy F           diffusion coefficients                 [0.1 0.1]\n"
+      "  --converge              enable the convergence test\n"
+      "  --check-interval N      steps between convergence checks       [20]\n"
+      "  --eps F                 convergence threshold on max|delta|    [1e-3]\n"
+      "  --backend cpu|hip       compute backend                        [hip if a GPU exists]\n"
+      "  --threads N             CPU OpenMP threads                     [runtime default]\n"
+      "  --kernel auto|naive|tb  GPU kernel family                      [auto]\n"
+      "  --tb-depth K            fused steps per pass (= halo depth)    [8 hip, 1 cpu]\n"
+      "  --decomp auto|rows|2d   process grid (auto = MPI_Dims_create)  [auto]\n"
+      "  --px P --py Q           explicit process grid\n"
+      "  --init ref-wrap|exact|random|zero  initial condition          [ref-wrap]\n"
+      "  --seed S                seed for --init random\n"
+      "  --out PATH|none         output file                            [per --naming]\n"
+      "  --out-format dat|bin|checksum                                  [dat]\n"
+      "  --naming plain|mpi|cuda reference-style file names and messages [plain]\n"
+      "  --dump-initial          also write the initial grid\n"
+      "  --compat none|mpi|cuda  reference step-count/check semantics   [none]\n"
+      "  --no-graph --no-overlap disable hipGraph capture / comm overlap\n"
+      "  --checkpoint PATH --checkpoint-every K   periodic binary checkpoints\n"
+      "  --resume PATH           start from a binary checkpoint\n"
+      "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
+      "  --port P                rendezvous port (default MASTER_PORT+1 or 29600)\n"
+      "  --json                  print a JSON metrics line\n");
+}
+
+int env_i(const char* n, int d) {
+  const char* v = std::getenv(n);
+  return v && *v ? std::atoi(v) : d;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Params P;
+  int64_t steps = 10000;
+  std::string out, out_format = "dat", naming = "plain", transport = "auto";
+  std::string checkpoint, resume;
+  int64_t ckpt_every = 0;
+  bool json = false, dump_initial = false, backend_set = false;
+  int port = 0;
+  std::map<std::string, std::string> kv;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto need = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", a.c_str());
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") { usage(); return 0; }
+    else if (a == "--nx") P.nx = std::atoll(need().c_str());
+    else if (a == "--ny") P.ny = std::atoll(need().c_str());
+    else if (a == "--steps") steps = std::atoll(need().c_str());
+    else if (a == "--cx") P.cx = float(std::atof(need().c_str()));
+    else if (a == "--cy") P.cy = float(std::atof(need().c_str()));
+    else if (a == "--converge") P.converge = true;
+    else if (a == "--check-interval") P.check_interval = std::atoi(need().c_str());
+    else if (a == "--eps") P.eps = float(std::atof(need().c_str()));
+    else if (a == "--backend") {
+      std::string b = need();
+      backend_set = true;
+      if (b == "cpu" || b == "serial" || b == "omp") P.backend = Backend::Cpu;
+      else if (b == "hip" || b == "gpu") P.backend = Backend::Hip;
+      else { std::fprintf(stderr, "bad backend %s\n", b.c_str()); return 2; }
+      if (b == "serial") P.threads = 1;
+    } else if (a == "--threads") P.threads = std::atoi(need().c_str());
+    else if (a == "--kernel") {
+      std::string k = need();
+      P.kernel = k == "naive" ? KernelKind::Naive : k == "tb" ? KernelKind::TB : KernelKind::Auto;
+    } else if (a == "--tb-depth") P.tb_depth = std::atoi(need().c_str());
+    else if (a == "--decomp") {
+      std::string d = need();
+      P.decomp = d == "rows" || d == "1d" ? DecompKind::Rows : d == "2d" ? DecompKind::Grid2D : DecompKind::Auto;
+    } else if (a == "--px") P.px = std::atoi(need().c_str());
+    else if (a == "--py") P.py = std::atoi(need().c_str());
+    else if (a == "--init") {
+      std::string m = need();
+      P.init = m == "exact" || m == "ref64" ? InitMode::Exact
+               : m == "random"              ? InitMode::Random
+               : m == "zero"                ? InitMode::Zero
+                                            : InitMode::RefWrap;
+    } else if (a == "--seed") P.seed = std::strtoull(need().c_str(), nullptr, 10);
+    else if (a == "--out") out = need();
+    else if (a == "--out-format") out_format = need();
+    else if (a == "--naming") naming = need();
+    else if (a == "--dump-initial") dump_initial = true;
+    else if (a == "--compat") {
+      std::string c = need();
+      P.compat = c == "mpi" ? Compat::Mpi : c == "cuda" ? Compat::Cuda : Compat::None;
+    } else if (a == "--no-graph") P.use_graph = false;
+    else if (a == "--graph") P.use_graph = true;
+    else if (a == "--no-overlap") P.overlap = false;
+    else if (a == "--overlap") P.overlap = true;
+    else if (a == "--checkpoint") checkpoint = need();
+    else if (a == "--checkpoint-every") ckpt_every = std::atoll(need().c_str());
+    else if (a == "--resume") resume = need();
+    else if (a == "--transport") transport = need();
+    else if (a == "--port") port = std::atoi(need().c_str());
+    else if (a == "--json") json = true;
+    else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
+  }
+  if (naming == "mpi" && P.compat == Compat::None) P.compat = Compat::Mpi;
+  if (naming == "cuda" && P.compat == Compat::None) P.compat = Compat::Cuda;
+
+  const int world = env_i("WORLD_SIZE", 1), rank = env_i("RANK", 0);
+  const int local_rank = env_i("LOCAL_RANK", rank);
+  const char* maddr = std::getenv("MASTER_ADDR");
+  const std::string addr = maddr && *maddr ? maddr : "127.0.0.1";
+  if (port == 0) port = env_i("HEAT_PORT", env_i("MASTER_PORT", 29599) + 1);
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  if (!backend_set) P.backend = ndev > 0 ? Backend::Hip : Backend::Cpu;
+  if (P.backend == Backend::Hip && ndev == 0) {
+    std::fprintf(stderr, "heat: --backend hip requested but no GPU is visible\n");
+    return 1;
+  }
+  if (P.backend == Backend::Hip) P.device = local_rank % ndev;
+
+  try {
+    std::unique_ptr<Transport> tr;
+    if (world == 1 || transport == "local") {
+      tr = make_local_transport();
+    } else if (P.backend == Backend::Hip && transport != "tcp") {
+      // Rendezvous over TCP, then RCCL.
+      unsigned char uid[128] = {0};
+      {
+        auto boot = make_tcp_transport(rank, world, addr, port);
+        if (rank == 0) {
+          rccl_unique_id(uid);
+          std::vector<Msg> m;
+          for (int r = 1; r < world; ++r) m.push_back(Msg{r, uid, 128, nullptr, 0});
+          boot->sendrecv(m.data(), int(m.size()), nullptr);
+        } else {
+          Msg m{0, nullptr, 0, uid, 128};
+          boot->sendrecv(&m, 1, nullptr);
+        }
+        boot->barrier();
+      }
+      tr = make_rccl_transport(rank, world, uid, P.device);
+    } else {
+      tr = make_tcp_transport(rank, world, addr, port);
+    }
+    const bool root = rank == 0;
+
+    // Reference-style banners (mpi/...c:90-96).
+    if (root && naming == "mpi") {
+      std::printf("Starting mpi_heat2D with %d worker tasks.\n", world);
+      if (!P.converge)
+        std::printf("Grid size: X= %lld  Y= %lld  Time steps= %lld\n", (long long)P.nx,
+                    (long long)P.ny, (long long)steps);
+      else
+        std::printf("Grid size: X= %lld  Y= %lld  Time steps= - \n", (long long)P.nx,
+                    (long long)P.ny);
+      std::fflush(stdout);
+    }
+
+    const double t_init0 = 0;
+    (void)t_init0;
+    Solver S(P, std::move(tr));
+    if (!resume.empty()) S.read_bin(resume);
+
+    const bool small = P.nx * P.ny <= (int64_t(1) << 24);
+    std::string init_path, final_path;
+    if (naming == "mpi") {
+      init_path = "initial_im.dat";
+      final_path = "final_im.dat";
+    } else if (naming == "cuda") {
+      // out_cuda_<TPB>_<NB>_<STEPS>.dat with the reference's geometry
+      // (THREADS_PER_ROW 32, cuda/cuda_heat.cu:17-21, :245-250).
+      const int64_t T = 32;
+      const int64_t rb = (P.nx - 2) / T + ((P.nx - 2) % T ? 1 : 0);
+      const int64_t cb = (P.ny - 2) / T + ((P.ny - 2) % T ? 1 : 0);
+      final_path = strprintf("out_cuda_%lld_%lld_%lld.dat", (long long)(T * T),
+                             (long long)(rb * cb), (long long)steps);
+    } else {
+      final_path = small ? "final.dat" : "none";
+      init_path = "initial.dat";
+    }
+    if (!out.empty()) final_path = out;
+
+    auto emit = [&](const std::string& path) {
+      if (path == "none" || path.empty()) return;
+      if (out_format == "bin") {
+        S.write_bin(path);
+      } else if (out_format == "checksum") {
+        Checksum c = S.checksum();
+        if (root) {
+          FILE* f = std::fopen(path.c_str(), "w");
+          HEAT_CHECK(f, "cannot open %s", path.c_str());
+          std::fprintf(f,
+                       "{\"nx\": %lld, \"ny\": %lld, \"step\": %lld, \"hash\": \"%016llx\", "
+                       "\"sum\": %.17g, \"min\": %.9g, \"max\": %.9g, \"count\": %lld}\n",
+                       (long long)P.nx, (long long)P.ny, (long long)S.step(),
+                       (unsigned long long)c.hash, c.sum, c.min, c.max, (long long)c.count);
+          std::fclose(f);
+        }
+      } else {
+        auto g = S.gather_root();
+        if (root) write_dat(path, P.nx, P.ny, g.data());
+      }
+    };
+    if (dump_initial || naming == "mpi") emit(init_path);
+
+    const int64_t total = S.configured_steps(steps);
+    int64_t todo = total - S.step();
+    RunStats acc;
+    while (todo > 0) {
+      const int64_t chunk = ckpt_every > 0 ? std::min(ckpt_every, todo) : todo;
+      RunStats r = S.run(chunk);
+      acc.steps_done += r.steps_done;
+      acc.seconds += r.seconds;
+      acc.passes += r.passes;
+      acc.exchanges += r.exchanges;
+      acc.checks += r.checks;
+      acc.last_resid = r.last_resid;
+      todo -= r.steps_done;
+      if (!checkpoint.empty() && ckpt_every > 0) S.write_bin(checkpoint);
+      if (r.converged) {
+        acc.converged = true;
+        acc.converged_at = r.converged_at;
+        break;
+      }
+    }
+    emit(final_path);
+
+    if (root) {
+      if (P.converge) {
+        if (naming == "mpi") {
+          if (acc.converged) std::printf("Converged after %lld steps\n", (long long)(acc.converged_at - 1));
+          else std::printf("Didn't converged\n");
+        } else if (naming == "cuda") {
+          if (acc.converged) std::printf("Converged at %lld steps\n", (long long)(acc.converged_at - 1));
+          else std::printf("Did not converge\n");
+        } else {
+          if (acc.converged) std::printf("Converged after %lld steps\n", (long long)acc.converged_at);
+          else std::printf("Did not converge after %lld steps\n", (long long)S.step());
+        }
+      }
+      const double secs = acc.seconds;
+      if (naming == "cuda") {
+        const double ms = secs * 1e3;
+        std::printf("Elapsed time: %.3f %ssecs\n", ms / 1000 > 1.0 ? ms / 1000 : ms,
+                    ms / 1000 > 1.0 ? "" : "m");
+      } else {
+        std::printf("Elapsed time %f secs\n", secs);
+      }
+      const double cells = double(P.nx) * double(P.ny) * double(acc.steps_done);
+      if (json) {
+        const auto& c = S.cart();
+        std::printf(
+            "{\"nx\": %lld, \"ny\": %lld, \"steps\": %lld, \"steps_done\": %lld, \"ranks\": %d, "
+            "\"backend\": \"%s\", \"decomp\": \"%dx%d\", \"tb_depth\": %d, \"seconds\": %.6f, "
+            "\"mcells_per_s\": %.3f, \"s_per_1000_iters\": %.6f, \"converged\": %s, "
+            "\"converged_at\": %lld, \"last_resid\": %.6g, \"passes\": %lld, \"exchanges\": %lld, "
+            "\"transport\": \"%s\"}\n",
+            (long long)P.nx, (long long)P.ny, (long long)total, (long long)acc.steps_done, world,
+            P.backend == Backend::Hip ? "hip" : "cpu", c.px, c.py, S.tb_depth(), secs,
+            secs > 0 ? cells / secs / 1e6 : 0.0,
+            acc.steps_done > 0 ? secs * 1000.0 / double(acc.steps_done) : 0.0,
+            acc.converged ? "true" : "false", (long long)acc.converged_at, double(acc.last_resid),
+            (long long)acc.passes, (long long)acc.exchanges, S.transport().name());
+      }
+      std::fflush(stdout);
+    }
+    S.barrier();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "heat: error: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -1,0 +1,138 @@
+/* C ABI of libheat.so — consumed by the Python package (ctypes) and usable
+ * from any language.  All functions return 0 on success and -1 on error;
+ * heat_last_error() then returns a thread-local message.
+ *
+ * Two layers:
+ *   heat_solver_*  the full per-rank engine (fields, passes, exchange, graphs)
+ *   heat_op_*      single kernels on caller-owned device buffers, for tests
+ *                  and for composing custom schedules (stream = hipStream_t).
+ */
+#ifndef HEAT_CAPI_H
+#define HEAT_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HEAT_ABI_VERSION 1
+
+typedef struct heat_params {
+  int64_t nx, ny;
+  float cx, cy;
+  int32_t converge, check_interval;
+  float eps;
+  int32_t init;      /* heat::InitMode */
+  uint64_t seed;
+  int32_t backend;   /* 0 cpu, 1 hip */
+  int32_t kernel;    /* 0 auto, 1 naive, 2 tb */
+  int32_t tb_depth;
+  int32_t threads;
+  int32_t decomp;    /* 0 auto(2-D), 1 rows, 2 grid2d */
+  int32_t px, py;
+  int32_t use_graph, overlap;
+  int32_t compat;    /* 0 none, 1 mpi, 2 cuda */
+  int32_t device;
+} heat_params;
+
+/* Transport selection for heat_solver_create. */
+typedef struct heat_comm {
+  int32_t kind;          /* 0 local, 1 rccl, 2 tcp, 3 callback */
+  int32_t rank, world;
+  int32_t device;        /* rccl: HIP device */
+  uint8_t unique_id[128];/* rccl: ncclUniqueId from heat_rccl_unique_id on rank 0 */
+  const char* addr;      /* tcp: rank-0 address */
+  int32_t port;          /* tcp: rank-0 port */
+  /* callback transport */
+  void* ctx;
+  int (*sendrecv)(void* ctx, const void* msgs /* heat_msg[n] */, int n);
+  int (*allreduce)(void* ctx, void* buf, int count, int dtype);
+  int (*barrier)(void* ctx);
+} heat_comm;
+
+typedef struct heat_run_stats {
+  int64_t steps_done, total_steps;
+  int32_t converged;
+  int64_t converged_at;
+  float last_resid;
+  double seconds;
+  int64_t passes, exchanges, checks;
+} heat_run_stats;
+
+typedef struct heat_block_info {
+  int32_t rank, world, px, py, cx, cy;
+  int64_t ox, oy, lx, ly;
+  int32_t nbr[4]; /* north, south, west, east; -1 = none */
+  int64_t pitch, rows;
+  int32_t hx, hy, halo, tb_depth;
+  int64_t bytes_per_field;
+} heat_block_info;
+
+typedef struct heat_checksum {
+  uint64_t hash;
+  double sum, min, max;
+  int64_t count;
+} heat_checksum;
+
+typedef struct heat_solver heat_solver;
+
+const char* heat_last_error(void);
+int heat_abi_version(void);
+const char* heat_build_info(void);
+
+int heat_rccl_unique_id(uint8_t out[128]);
+int heat_device_count(int* n);
+
+int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out);
+int heat_solver_destroy(heat_solver* s);
+int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
+int heat_solver_reset(heat_solver* s);
+int heat_solver_info(heat_solver* s, heat_block_info* out);
+int heat_solver_step(heat_solver* s, int64_t* out);
+int heat_solver_copy_owned(heat_solver* s, float* host, int64_t host_pitch);
+int heat_solver_load_owned(heat_solver* s, const float* host, int64_t host_pitch, int64_t step);
+/* rank 0: host must hold nx*ny floats; other ranks: host may be NULL */
+int heat_solver_gather(heat_solver* s, float* host);
+int heat_solver_checksum(heat_solver* s, heat_checksum* out);
+int heat_solver_write_bin(heat_solver* s, const char* path);
+int heat_solver_read_bin(heat_solver* s, const char* path);
+int heat_solver_barrier(heat_solver* s);
+int heat_solver_current_ptr(heat_solver* s, void** ptr);
+
+/* host utilities */
+int heat_write_dat(const char* path, int64_t nx, int64_t ny, const float* grid);
+int heat_format_6_1f(float v, char* out, int cap);
+int heat_dims_create(int nnodes, int ndims, int* dims);
+int heat_block_span(int64_t n, int parts, int index, int64_t* offset, int64_t* size);
+int heat_init_value(int mode, int64_t ix, int64_t iy, int64_t nx, int64_t ny, uint64_t seed,
+                    float* out);
+int heat_cpu_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0, int64_t nx,
+                  int64_t ny, float cx, float cy, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                  float* resid /* may be NULL */);
+
+/* device ops (pointers are device pointers to local cell (0,0); stream is a hipStream_t) */
+int heat_op_naive_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
+                       int64_t nx, int64_t ny, float cx, float cy, int64_t r0, int64_t r1,
+                       int64_t c0, int64_t c1, unsigned* resid, void* stream);
+int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
+                    int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
+                    int nbox, int depth, unsigned* resid, void* stream, int waves_target);
+int heat_op_init(float* origin, int64_t lx, int64_t ly, int halo, int64_t gx0, int64_t gy0,
+                 int64_t nx, int64_t ny, int mode, uint64_t seed, void* stream);
+int heat_op_pack(const float* origin, int64_t pitch, int64_t r0, int64_t r1, int64_t c0,
+                 int64_t c1, float* buf, void* stream);
+int heat_op_unpack(const float* buf, float* origin, int64_t pitch, int64_t r0, int64_t r1,
+                   int64_t c0, int64_t c1, void* stream);
+int heat_op_residual(const float* a, const float* b, int64_t pitch, int64_t r0, int64_t r1,
+                     int64_t c0, int64_t c1, unsigned* resid, void* stream);
+int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows, int* hx,
+                int* hy);
+int heat_tb_supported(int depth);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEAT_CAPI_H */

@@ -1,0 +1,67 @@
+// Device kernel launchers (gfx950).  Implementations: csrc/kernels/*.hip.
+//
+// Reference kernels these replace:
+//   heat(old,new)              cuda/cuda_heat.cu:140-163  -> naive_step / tb_step
+//   heat<threads>(old,new,f)   cuda/cuda_heat.cu:42-138   -> the same kernels with the
+//                                                           fused max|delta| residual
+//   semi_reduce(f)             cuda/cuda_heat.cu:32-40    -> removed: the residual is a
+//                                                           single device word (atomic max)
+//   MPI col_type datatype      mpi/...c:82-84             -> pack_box / unpack_box
+//   host inidat + H2D copies   cuda/cuda_heat.cu:194-198  -> init_field (device side)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "heat/topology.hpp"
+
+namespace heat::gpu {
+
+// Geometry shared by all stencil kernels.  `src`/`dst` point at local owned
+// cell (0,0) of a field allocated with some Layout; (gx0, gy0) are the
+// global coordinates of that cell.  Only cells with 1 <= gx <= nx-2 and
+// 1 <= gy <= ny-2 are updated (fixed Dirichlet ring); every other
+// cell keeps its value.
+struct StencilGeom {
+  int64_t pitch = 0;
+  int64_t gx0 = 0, gy0 = 0;
+  int64_t nx = 0, ny = 0;
+  float cx = 0.1f, cy = 0.1f;
+};
+
+// Depths the temporally blocked kernel is instantiated for.
+constexpr int kTbMaxDepth = 16;
+bool tb_depth_supported(int k);
+// Output columns per 256-column strip at depth k.
+int tb_strip_width(int k);
+
+// Fill every allocated cell (owned, ghost ring and padding) of a field with
+// the initial condition at its global coordinates (0 outside the plate).
+void init_field(float* origin, const Layout& L, int64_t gx0, int64_t gy0, int64_t nx,
+                int64_t ny, int mode, uint64_t seed, hipStream_t st);
+
+// One Jacobi step over `box` (local coordinates), one cell per thread.
+// If resid != nullptr, atomically max-reduces |new - old| (as float bits)
+// over the box into *resid.
+void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
+                unsigned* resid, hipStream_t st);
+
+// `depth` fused Jacobi steps over up to 5 output boxes in one launch using
+// the register-streaming temporally blocked kernel.  Reads rows
+// [r0-depth, r1+depth) and columns [c0-round_up(depth,4), ...) of src, so the
+// ghost ring must be at least that deep and valid (halo exchanged).
+// Box column starts must be multiples of 4.  `waves_target` steers the row
+// chunking (parallelism vs. redundant halo work).
+void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
+             int depth, unsigned* resid, hipStream_t st, int waves_target = 0);
+
+// Copy a box of a strided field to/from a contiguous buffer (E/W halos).
+void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hipStream_t st);
+void unpack_box(const float* buf, float* origin, int64_t pitch, const Box& box, hipStream_t st);
+
+// Max |a-b| over a box (standalone residual), atomically into *resid.
+void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,
+                  hipStream_t st);
+
+}  // namespace heat::gpu

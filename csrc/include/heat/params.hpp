@@ -1,0 +1,74 @@
+// Run-time configuration of a heat-diffusion run.
+//
+// The reference fixes everything at compile time with -D macros
+// (cuda/cuda_heat.cu:7-23, mpi/mpi_heat_improved_persistent_stat.c:7-32,
+// mpi/Makefile:1-25).  Here the same knobs are run-time fields; the defaults
+// reproduce the reference's source defaults (20x20 grid, cx=cy=0.1,
+// eps=1e-3, check interval 20 as in cuda/cuda_heat.cu:16 / mpi/Makefile:8).
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+namespace heat {
+
+// Initial condition (reference: inidat, cuda/cuda_heat.cu:274-280).
+enum class InitMode : int {
+  RefWrap = 0,  // ix*(nx-ix-1)*iy*(ny-iy-1) in int32 with two's-complement wrap
+                // (bit-identical to what the reference binaries compute)
+  Exact = 1,    // the same polynomial evaluated exactly (fp64), then rounded
+  Random = 2,   // counter-based hash of (seed, gx, gy) -> [0, 100): independent
+                // of the decomposition
+  Zero = 3,
+};
+
+enum class Backend : int { Cpu = 0, Hip = 1 };
+
+// Stencil kernel family on the GPU.
+enum class KernelKind : int {
+  Auto = 0,   // temporally blocked streaming kernel (TB) at the tuned depth
+  Naive = 1,  // one cell per thread, global loads only (independent oracle)
+  TB = 2,     // register-streaming temporally blocked kernel, depth tb_depth
+};
+
+// Reference-compatibility switches.
+enum class Compat : int {
+  None = 0,  // exactly `steps` updates; check after steps C, 2C, ...; converged <=> max|d| < eps
+  Mpi = 1,   // steps+1 updates; check after C, 2C, ...; converged <=> max|d| <= eps
+  Cuda = 2,  // steps updates; check after 1, C+1, 2C+1, ...; converged <=> max|d| < eps
+};
+
+// How the process grid is formed from the world size.
+enum class DecompKind : int {
+  Auto = 0,  // 2-D, MPI_Dims_create-compatible (mpi/...c:51-52)
+  Rows = 1,  // 1-D slabs along x (contiguous halo rows, no packing)
+  Grid2D = 2,
+};
+
+struct Params {
+  int64_t nx = 20;  // rows (slow index), NXPROB
+  int64_t ny = 20;  // columns (contiguous index), NYPROB
+  float cx = 0.1f;  // PARMS_CX / parms.cx
+  float cy = 0.1f;  // PARMS_CY / parms.cy
+  bool converge = false;   // -DCONVERGE
+  int check_interval = 20; // CHECK_INTERVAL / STEP
+  float eps = 1e-3f;       // literal 1e-3 of the reference
+  InitMode init = InitMode::RefWrap;
+  uint64_t seed = 0;
+  Backend backend = Backend::Cpu;
+  KernelKind kernel = KernelKind::Auto;
+  int tb_depth = 0;     // 0 = tuned default
+  int threads = 0;      // CPU OpenMP threads (0 = runtime default)
+  DecompKind decomp = DecompKind::Auto;
+  int px = 0, py = 0;   // explicit process grid (0 = derived)
+  bool use_graph = true;    // capture step chunks as hipGraphs
+  bool overlap = true;      // halo exchange concurrent with interior compute
+  Compat compat = Compat::None;
+  int device = -1;          // HIP device ordinal (-1 = local rank % device count)
+};
+
+const char* init_mode_name(InitMode m);
+const char* kernel_name(KernelKind k);
+const char* compat_name(Compat c);
+
+}  // namespace heat

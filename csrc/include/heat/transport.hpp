@@ -1,0 +1,98 @@
+// Inter-rank transports for halo exchange, residual all-reduce and gather.
+//
+// The reference does all of this with MPI: persistent
+// non-blocking halo sends/receives (mpi/...c:130-161, :177, :263), one
+// MPI_Allreduce(LAND) per convergence check (:255) and row-by-row
+// scatter/gather through rank 0 (:100-127, :270-297).
+//
+// Here one process drives one GPU and the transport is pluggable:
+//   LocalTransport     world of one (no messages).
+//   RcclTransport      RCCL over xGMI: grouped ncclSend/ncclRecv on a comm
+//                      stream, ncclAllReduce(max); device buffers,
+//                      stream-ordered and hipGraph-capturable.  The unique
+//                      id is produced by rank 0 and distributed by the
+//                      caller (torch.distributed store or the TCP bootstrap).
+//   TcpTransport       host memory over TCP sockets: the CPU multi-process
+//                      backend of the standalone `heat` binary (the MPI
+//                      program's role) and the RCCL bootstrap.
+//   CallbackTransport  host memory; the wire is supplied by the embedding
+//                      program (the Python package routes it through
+//                      torch.distributed, e.g. gloo on CPU).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace heat {
+
+// One peer exchange: send sbytes from sbuf to `peer` and receive rbytes
+// from the same peer into rbuf.  Either side may be empty.
+struct Msg {
+  int peer = -1;
+  const void* sbuf = nullptr;
+  size_t sbytes = 0;
+  void* rbuf = nullptr;
+  size_t rbytes = 0;
+};
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  // true: buffers are device pointers and operations are ordered on `st`
+  // (asynchronous); false: host buffers, operations complete on return.
+  virtual bool device_memory() const = 0;
+  virtual bool graph_capturable() const { return false; }
+  // All messages of one call progress concurrently (grouped).
+  virtual void sendrecv(const Msg* msgs, int n, hipStream_t st) = 0;
+  // In-place max over ranks of `count` floats.
+  virtual void allreduce_max(float* buf, int count, hipStream_t st) = 0;
+  // In-place sum over ranks of `count` doubles / uint64 (host or device per device_memory()).
+  virtual void allreduce_sum_f64(double* buf, int count, hipStream_t st) = 0;
+  virtual void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) = 0;
+  virtual void barrier() = 0;
+  virtual const char* name() const = 0;
+};
+
+std::unique_ptr<Transport> make_local_transport();
+
+// RCCL: `unique_id` is the 128-byte ncclUniqueId produced by rcclUniqueId()
+// on rank 0 and broadcast by the caller.
+std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const void* unique_id,
+                                               int device);
+// Writes a fresh ncclUniqueId (128 bytes) into out.
+void rccl_unique_id(void* out128);
+
+// TCP: rank 0 listens on (addr, port); everyone connects to everyone
+// (full mesh, one socket per peer pair).
+std::unique_ptr<Transport> make_tcp_transport(int rank, int world, const std::string& addr,
+                                              int port);
+
+// Callback transport (C ABI so foreign runtimes can implement it).
+extern "C" {
+struct heat_msg {
+  int peer;
+  const void* sbuf;
+  size_t sbytes;
+  void* rbuf;
+  size_t rbytes;
+};
+struct heat_callbacks {
+  void* ctx;
+  int rank;
+  int world;
+  // return 0 on success
+  int (*sendrecv)(void* ctx, const heat_msg* msgs, int n);
+  int (*allreduce)(void* ctx, void* buf, int count, int dtype /*0 f32 max, 1 f64 sum, 2 u64 sum*/);
+  int (*barrier)(void* ctx);
+};
+}
+std::unique_ptr<Transport> make_callback_transport(const heat_callbacks& cb);
+
+}  // namespace heat

@@ -1,0 +1,639 @@
+// Per-rank solver runtime (see solver.hpp for the design and reference map).
+#include "heat/solver.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "heat/common.hpp"
+#include "heat/cpu_backend.hpp"
+#include "heat/kernels.hpp"
+
+namespace heat {
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int env_int(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+
+// Host-side box <-> contiguous copies for the CPU backend's E/W halos.
+void host_pack(const float* origin, int64_t pitch, const Box& b, float* buf) {
+  for (int64_t r = b.r0; r < b.r1; ++r)
+    std::memcpy(buf + (r - b.r0) * b.cols(), origin + r * pitch + b.c0, size_t(b.cols()) * 4);
+}
+void host_unpack(const float* buf, float* origin, int64_t pitch, const Box& b) {
+  for (int64_t r = b.r0; r < b.r1; ++r)
+    std::memcpy(origin + r * pitch + b.c0, buf + (r - b.r0) * b.cols(), size_t(b.cols()) * 4);
+}
+
+}  // namespace
+
+Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std::move(tr)) {
+  HEAT_CHECK(tr_ != nullptr, "no transport");
+  HEAT_CHECK(P_.nx >= 1 && P_.ny >= 1, "grid %lldx%lld", (long long)P_.nx, (long long)P_.ny);
+  HEAT_CHECK(P_.check_interval >= 1, "check interval %d", P_.check_interval);
+  cart_ = Cart(tr_->world(), P_.decomp, P_.px, P_.py, P_.nx, P_.ny);
+  blk_ = make_block(cart_, tr_->rank(), P_.nx, P_.ny);
+  if (on_gpu()) {
+    if (P_.kernel == KernelKind::Naive) {
+      T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
+    } else {
+      T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 8);
+      HEAT_CHECK(gpu::tb_depth_supported(T_), "TB depth %d not supported", T_);
+    }
+    HEAT_CHECK(!(tr_->device_memory() && tr_->world() > 1) || true, "");
+  } else {
+    HEAT_CHECK(!tr_->device_memory(), "transport %s needs the GPU backend", tr_->name());
+    T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
+    cpu::set_threads(P_.threads);
+  }
+  H_ = T_;
+  // A rank must own at least H rows/columns along every decomposed axis so
+  // that a k-deep halo comes from its direct neighbour only.
+  HEAT_CHECK(cart_.px == 1 || blk_.lx >= H_, "block of %lld rows is thinner than halo depth %d",
+             (long long)blk_.lx, H_);
+  HEAT_CHECK(cart_.py == 1 || blk_.ly >= H_, "block of %lld cols is thinner than halo depth %d",
+             (long long)blk_.ly, H_);
+  L_ = Layout::make(blk_.lx, blk_.ly, H_);
+  staged_ = on_gpu() && !tr_->device_memory() && tr_->world() > 1;
+  alloc();
+  init_fields();
+}
+
+Solver::~Solver() { free_all(); }
+
+void Solver::alloc() {
+  const size_t ew_elems = size_t(blk_.lx) * size_t(H_);
+  if (on_gpu()) {
+    const int dev = P_.device >= 0 ? P_.device : 0;
+    HIP_CHECK(hipSetDevice(dev));
+    for (int i = 0; i < 2; ++i) {
+      HIP_CHECK(hipMalloc(&base_[i], size_t(L_.bytes())));
+      field_[i] = base_[i] + L_.origin();
+    }
+    if (cart_.py > 1)
+      for (auto& b : ew_) HIP_CHECK(hipMalloc(&b, ew_elems * 4));
+    HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreate(&ev_t0_));
+    HIP_CHECK(hipEventCreate(&ev_t1_));
+    HIP_CHECK(hipMalloc(&d_resid_, 256));
+    HIP_CHECK(hipHostMalloc(&h_resid_, 256));
+    HIP_CHECK(hipMalloc(&d_scratch_, 4096));
+    if (staged_) {
+      stage_bytes_ = std::max<size_t>(size_t(H_) * size_t(L_.pitch), ew_elems) * 4;
+      for (int i = 0; i < 4; ++i) {
+        HIP_CHECK(hipHostMalloc(&stage_send_[i], stage_bytes_));
+        HIP_CHECK(hipHostMalloc(&stage_recv_[i], stage_bytes_));
+      }
+    }
+  } else {
+    for (int i = 0; i < 2; ++i) {
+      base_[i] = static_cast<float*>(std::aligned_alloc(256, size_t(round_up(L_.bytes(), 256))));
+      HEAT_CHECK(base_[i] != nullptr, "host allocation of %lld bytes failed",
+                 (long long)L_.bytes());
+      field_[i] = base_[i] + L_.origin();
+    }
+    if (cart_.py > 1)
+      for (auto& b : ew_) {
+        b = static_cast<float*>(std::malloc(ew_elems * 4));
+        HEAT_CHECK(b != nullptr, "host allocation failed");
+      }
+  }
+}
+
+void Solver::free_all() {
+  if (on_gpu()) {
+    if (s_comp_) (void)hipStreamSynchronize(s_comp_);
+    if (s_comm_) (void)hipStreamSynchronize(s_comm_);
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second.exec);
+    graphs_.clear();
+    for (auto& b : base_)
+      if (b) (void)hipFree(b);
+    for (auto& b : ew_)
+      if (b) (void)hipFree(b);
+    for (int i = 0; i < 4; ++i) {
+      if (stage_send_[i]) (void)hipHostFree(stage_send_[i]);
+      if (stage_recv_[i]) (void)hipHostFree(stage_recv_[i]);
+    }
+    if (d_resid_) (void)hipFree(d_resid_);
+    if (h_resid_) (void)hipHostFree(h_resid_);
+    if (d_scratch_) (void)hipFree(d_scratch_);
+    for (auto e : {ev_ready_, ev_halo_, ev_t0_, ev_t1_})
+      if (e) (void)hipEventDestroy(e);
+    if (s_comp_) (void)hipStreamDestroy(s_comp_);
+    if (s_comm_) (void)hipStreamDestroy(s_comm_);
+  } else {
+    for (auto& b : base_) std::free(b);
+    for (auto& b : ew_) std::free(b);
+  }
+  for (auto& b : base_) b = nullptr;
+  for (auto& b : ew_) b = nullptr;
+}
+
+void Solver::init_fields() {
+  const int mode = int(P_.init);
+  for (int i = 0; i < 2; ++i) {
+    if (on_gpu())
+      gpu::init_field(field_[i], L_, blk_.ox, blk_.oy, P_.nx, P_.ny, mode, P_.seed, s_comp_);
+    else
+      cpu::init_field(field_[i], L_, blk_.ox, blk_.oy, P_.nx, P_.ny, mode, P_.seed);
+  }
+  if (on_gpu()) HIP_CHECK(hipStreamSynchronize(s_comp_));
+  cur_ = 0;
+  step_ = 0;
+}
+
+void Solver::reset() { init_fields(); }
+
+int64_t Solver::configured_steps(int64_t steps) const {
+  return P_.compat == Compat::Mpi ? steps + 1 : steps;
+}
+
+std::vector<int> Solver::pass_depths(int64_t n) const {
+  std::vector<int> d;
+  const bool tb = on_gpu() && P_.kernel != KernelKind::Naive;
+  while (n > 0) {
+    int k = int(std::min<int64_t>(T_, n));
+    if (tb)
+      while (!gpu::tb_depth_supported(k)) --k;
+    d.push_back(k);
+    n -= k;
+  }
+  return d;
+}
+
+// ---------------------------------------------------------------------------
+// halo exchange
+// ---------------------------------------------------------------------------
+void Solver::exchange(int buf, int k, hipStream_t st) {
+  float* f = field_[buf];
+  const auto& nb = blk_.nbr;
+  const int64_t lx = blk_.lx, ly = blk_.ly, pitch = L_.pitch;
+  const bool gpu = on_gpu();
+
+  auto do_sendrecv = [&](std::vector<Msg>& msgs) {
+    if (msgs.empty()) return;
+    if (!staged_) {
+      tr_->sendrecv(msgs.data(), int(msgs.size()), st);
+      return;
+    }
+    // GPU fields, host transport: stage through pinned host memory.
+    std::vector<Msg> host(msgs.size());
+    for (size_t i = 0; i < msgs.size(); ++i) {
+      HEAT_CHECK(msgs[i].sbytes <= stage_bytes_ && msgs[i].rbytes <= stage_bytes_, "stage size");
+      host[i] = Msg{msgs[i].peer, stage_send_[i], msgs[i].sbytes, stage_recv_[i], msgs[i].rbytes};
+      if (msgs[i].sbytes)
+        HIP_CHECK(hipMemcpyAsync(stage_send_[i], msgs[i].sbuf, msgs[i].sbytes,
+                                 hipMemcpyDeviceToHost, st));
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    tr_->sendrecv(host.data(), int(host.size()), st);
+    for (size_t i = 0; i < msgs.size(); ++i)
+      if (msgs[i].rbytes)
+        HIP_CHECK(hipMemcpyAsync(msgs[i].rbuf, stage_recv_[i], msgs[i].rbytes,
+                                 hipMemcpyHostToDevice, st));
+  };
+
+  // Phase 1: west/east columns of the owned rows (packed).
+  if (nb[West] >= 0 || nb[East] >= 0) {
+    const size_t bytes = size_t(lx) * size_t(k) * 4;
+    const Box sw{0, lx, 0, k}, se{0, lx, ly - k, ly}, rw{0, lx, -k, 0}, re{0, lx, ly, ly + k};
+    std::vector<Msg> msgs;
+    if (nb[West] >= 0) {
+      if (gpu) gpu::pack_box(f, pitch, sw, ew_[0], st);
+      else host_pack(f, pitch, sw, ew_[0]);
+      msgs.push_back(Msg{nb[West], ew_[0], bytes, ew_[2], bytes});
+    }
+    if (nb[East] >= 0) {
+      if (gpu) gpu::pack_box(f, pitch, se, ew_[1], st);
+      else host_pack(f, pitch, se, ew_[1]);
+      msgs.push_back(Msg{nb[East], ew_[1], bytes, ew_[3], bytes});
+    }
+    do_sendrecv(msgs);
+    if (nb[West] >= 0) {
+      if (gpu) gpu::unpack_box(ew_[2], f, pitch, rw, st);
+      else host_unpack(ew_[2], f, pitch, rw);
+    }
+    if (nb[East] >= 0) {
+      if (gpu) gpu::unpack_box(ew_[3], f, pitch, re, st);
+      else host_unpack(ew_[3], f, pitch, re);
+    }
+  }
+  // Phase 2: north/south full padded rows (contiguous, no packing).  They
+  // include the just-received W/E ghost columns, which fills the corners
+  // that k > 1 deep halos need.
+  if (nb[North] >= 0 || nb[South] >= 0) {
+    const size_t bytes = size_t(k) * size_t(pitch) * 4;
+    const int64_t hy = L_.hy;
+    std::vector<Msg> msgs;
+    if (nb[North] >= 0)
+      msgs.push_back(Msg{nb[North], f - hy, bytes, f - k * pitch - hy, bytes});
+    if (nb[South] >= 0)
+      msgs.push_back(Msg{nb[South], f + (lx - k) * pitch - hy, bytes, f + lx * pitch - hy, bytes});
+    do_sendrecv(msgs);
+  }
+  ++stat_exchanges_;
+}
+
+// ---------------------------------------------------------------------------
+// compute
+// ---------------------------------------------------------------------------
+void Solver::compute_gpu(int k, bool resid, bool split, int part) {
+  const float* src = field_[cur_];
+  float* dst = field_[cur_ ^ 1];
+  gpu::StencilGeom g;
+  g.pitch = L_.pitch;
+  g.gx0 = blk_.ox;
+  g.gy0 = blk_.oy;
+  g.nx = P_.nx;
+  g.ny = P_.ny;
+  g.cx = P_.cx;
+  g.cy = P_.cy;
+  unsigned* r = resid ? d_resid_ : nullptr;
+  const int64_t lx = blk_.lx, ly = blk_.ly;
+  const auto& nb = blk_.nbr;
+  static const int waves_target = env_int("HEAT_TB_WAVES", 0);
+
+  if (P_.kernel == KernelKind::Naive) {
+    // k single steps over shrinking regions (deep halo), ping-ponging.
+    for (int j = 0; j < k; ++j) {
+      const int64_t e = k - 1 - j;
+      Box b{nb[North] >= 0 ? -e : 0, lx + (nb[South] >= 0 ? e : 0), nb[West] >= 0 ? -e : 0,
+            ly + (nb[East] >= 0 ? e : 0)};
+      const float* a = field_[cur_];
+      float* d = field_[cur_ ^ 1];
+      gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+      cur_ ^= 1;
+    }
+    return;
+  }
+
+  if (!split) {
+    Box full{0, lx, 0, ly};
+    gpu::tb_step(src, dst, g, &full, 1, k, r, s_comp_, waves_target);
+    return;
+  }
+  const int64_t r0 = nb[North] >= 0 ? k : 0, r1 = nb[South] >= 0 ? lx - k : lx;
+  const int64_t c0 = nb[West] >= 0 ? round_up(k, 4) : 0;
+  const int64_t c1 = nb[East] >= 0 ? round_down(ly - k, 4) : ly;
+  if (part == 0) {
+    Box in{r0, r1, c0, c1};
+    gpu::tb_step(src, dst, g, &in, 1, k, r, s_comp_, waves_target);
+  } else {
+    Box b[4] = {{0, r0, 0, ly}, {r1, lx, 0, ly}, {r0, r1, 0, c0}, {r0, r1, c1, ly}};
+    gpu::tb_step(src, dst, g, b, 4, k, r, s_comp_, waves_target);
+    // cur_ flips once per pass, after the boundary part.
+  }
+}
+
+void Solver::compute_cpu(int k, bool resid) {
+  cpu::Geom g;
+  g.pitch = L_.pitch;
+  g.gx0 = blk_.ox;
+  g.gy0 = blk_.oy;
+  g.nx = P_.nx;
+  g.ny = P_.ny;
+  g.cx = P_.cx;
+  g.cy = P_.cy;
+  const auto& nb = blk_.nbr;
+  for (int j = 0; j < k; ++j) {
+    const int64_t e = k - 1 - j;
+    Box b{nb[North] >= 0 ? -e : 0, blk_.lx + (nb[South] >= 0 ? e : 0), nb[West] >= 0 ? -e : 0,
+          blk_.ly + (nb[East] >= 0 ? e : 0)};
+    const bool last = j == k - 1;
+    float r = cpu::step(field_[cur_], field_[cur_ ^ 1], g, b, resid && last);
+    if (resid && last) cpu_resid_ = r;
+    cur_ ^= 1;
+  }
+}
+
+void Solver::enqueue_pass(int k, bool resid) {
+  const auto& nb = blk_.nbr;
+  const bool has_nbr = nb[0] >= 0 || nb[1] >= 0 || nb[2] >= 0 || nb[3] >= 0;
+  if (on_gpu()) {
+    if (resid) HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
+    const bool tb = P_.kernel != KernelKind::Naive;
+    const int64_t lx = blk_.lx, ly = blk_.ly;
+    const int64_t ir0 = nb[North] >= 0 ? k : 0, ir1 = nb[South] >= 0 ? lx - k : lx;
+    const int64_t ic0 = nb[West] >= 0 ? round_up(k, 4) : 0;
+    const int64_t ic1 = nb[East] >= 0 ? round_down(ly - k, 4) : ly;
+    const bool interior_ok = ir1 > ir0 && ic1 > ic0;
+    if (!has_nbr) {
+      compute_gpu(k, resid, false, 0);
+    } else if (tb && P_.overlap && !staged_ && interior_ok) {
+      HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+      exchange(cur_, k, s_comm_);
+      HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+      compute_gpu(k, resid, true, 0);
+      HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+      compute_gpu(k, resid, true, 1);
+    } else {
+      exchange(cur_, k, s_comp_);
+      compute_gpu(k, resid, false, 0);
+    }
+    if (tb) cur_ ^= 1;
+    if (resid) {
+      if (tr_->device_memory()) tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
+      HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
+    }
+  } else {
+    if (has_nbr) exchange(cur_, k, nullptr);
+    compute_cpu(k, resid);
+  }
+  step_ += k;
+  ++stat_passes_;
+}
+
+void Solver::enqueue_segment(int64_t n, bool resid) {
+  auto d = pass_depths(n);
+  for (size_t i = 0; i < d.size(); ++i) enqueue_pass(d[i], resid && i + 1 == d.size());
+}
+
+float Solver::finish_resid() {
+  float r;
+  if (on_gpu()) {
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    std::memcpy(&r, h_resid_, 4);
+    if (!tr_->device_memory()) tr_->allreduce_max(&r, 1, nullptr);
+  } else {
+    r = cpu_resid_;
+    tr_->allreduce_max(&r, 1, nullptr);
+  }
+  return r;
+}
+
+bool Solver::is_check_point(int64_t completed) const {
+  const int64_t C = P_.check_interval;
+  if (P_.compat == Compat::Cuda) return completed >= 1 && (completed - 1) % C == 0;
+  return completed >= 1 && completed % C == 0;
+}
+
+bool Solver::converged_value(float r) const {
+  return P_.compat == Compat::Mpi ? r <= P_.eps : r < P_.eps;
+}
+
+RunStats Solver::run(int64_t steps) {
+  RunStats s;
+  HEAT_CHECK(steps >= 0, "negative step count");
+  const int64_t p0 = stat_passes_, e0 = stat_exchanges_;
+  synchronize();
+  const double t0 = now_s();
+  const bool gpu = on_gpu();
+  const bool can_graph = gpu && P_.use_graph && !staged_ &&
+                         (tr_->world() == 1 || tr_->graph_capturable()) &&
+                         env_int("HEAT_GRAPH", 1) != 0;
+  static bool warmed = false;
+  if (can_graph && tr_->world() > 1 && !warmed) {
+    // Let RCCL establish its connections outside of stream capture.  A halo
+    // exchange of the current buffer is idempotent.
+    exchange(cur_, H_, s_comp_);
+    tr_->allreduce_max(reinterpret_cast<float*>(d_scratch_), 1, s_comp_);
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    warmed = true;
+  }
+  int64_t remaining = steps;
+  while (remaining > 0) {
+    int64_t seg = remaining;
+    bool resid = false;
+    if (P_.converge) {
+      int64_t next;
+      if (P_.compat == Compat::Cuda)
+        next = step_ < 1 ? 1 : ((step_ - 1) / P_.check_interval + 1) * P_.check_interval + 1;
+      else
+        next = (step_ / P_.check_interval + 1) * P_.check_interval;
+      if (next - step_ <= remaining) {
+        seg = next - step_;
+        resid = true;
+      }
+    }
+    if (can_graph) {
+      const auto key = std::make_tuple(seg, resid, cur_);
+      auto it = graphs_.find(key);
+      const int cur_before = cur_;
+      const int64_t step_before = step_;
+      if (it == graphs_.end()) {
+        const int64_t p_before = stat_passes_, e_before = stat_exchanges_;
+        hipGraph_t graph;
+        HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
+        capturing_ = true;
+        try {
+          enqueue_segment(seg, resid);
+        } catch (...) {
+          capturing_ = false;
+          hipGraph_t g2;
+          (void)hipStreamEndCapture(s_comp_, &g2);
+          throw;
+        }
+        capturing_ = false;
+        HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
+        GraphEntry e;
+        HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphDestroy(graph));
+        e.cur_after = cur_;
+        e.passes = stat_passes_ - p_before;
+        e.exchanges = stat_exchanges_ - e_before;
+        stat_passes_ = p_before;
+        stat_exchanges_ = e_before;
+        it = graphs_.emplace(key, e).first;
+      }
+      HIP_CHECK(hipGraphLaunch(it->second.exec, s_comp_));
+      cur_ = it->second.cur_after;
+      step_ = step_before + seg;
+      stat_passes_ += it->second.passes;
+      stat_exchanges_ += it->second.exchanges;
+      (void)cur_before;
+    } else {
+      enqueue_segment(seg, resid);
+    }
+    remaining -= seg;
+    s.steps_done += seg;
+    if (resid) {
+      const float r = finish_resid();
+      ++s.checks;
+      s.last_resid = r;
+      if (!(r == r) || std::isinf(r))
+        throw_error(__FILE__, __LINE__,
+                    strprintf("non-finite residual (%g) at step %lld", double(r), (long long)step_));
+      if (converged_value(r)) {
+        s.converged = true;
+        s.converged_at = step_;
+        break;
+      }
+    }
+  }
+  synchronize();
+  s.seconds = now_s() - t0;
+  s.total_steps = step_;
+  s.passes = stat_passes_ - p0;
+  s.exchanges = stat_exchanges_ - e0;
+  return s;
+}
+
+void Solver::synchronize() {
+  if (on_gpu()) {
+    HIP_CHECK(hipStreamSynchronize(s_comm_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// state access, gather, checksum, binary I/O
+// ---------------------------------------------------------------------------
+void Solver::copy_owned(float* host, int64_t host_pitch) {
+  if (on_gpu()) {
+    HIP_CHECK(hipMemcpy2DAsync(host, size_t(host_pitch) * 4, field_[cur_], size_t(L_.pitch) * 4,
+                               size_t(blk_.ly) * 4, size_t(blk_.lx), hipMemcpyDeviceToHost,
+                               s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+  } else {
+    for (int64_t r = 0; r < blk_.lx; ++r)
+      std::memcpy(host + r * host_pitch, field_[cur_] + r * L_.pitch, size_t(blk_.ly) * 4);
+  }
+}
+
+void Solver::load_owned(const float* host, int64_t host_pitch, int64_t step) {
+  synchronize();
+  for (int b = 0; b < 2; ++b) {
+    if (on_gpu()) {
+      HIP_CHECK(hipMemcpy2DAsync(field_[b], size_t(L_.pitch) * 4, host, size_t(host_pitch) * 4,
+                                 size_t(blk_.ly) * 4, size_t(blk_.lx), hipMemcpyHostToDevice,
+                                 s_comp_));
+    } else {
+      for (int64_t r = 0; r < blk_.lx; ++r)
+        std::memcpy(field_[b] + r * L_.pitch, host + r * host_pitch, size_t(blk_.ly) * 4);
+    }
+  }
+  synchronize();
+  step_ = step;
+}
+
+std::vector<float> Solver::gather_root() {
+  const int rank = tr_->rank(), world = tr_->world();
+  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+  copy_owned(mine.data(), blk_.ly);
+  std::vector<float> out;
+  const bool dev = tr_->device_memory();
+  int64_t max_block = 0;
+  for (int r = 0; r < world; ++r) {
+    Block b = make_block(cart_, r, P_.nx, P_.ny);
+    max_block = std::max(max_block, b.lx * b.ly);
+  }
+  float* dbuf = nullptr;
+  if (dev && world > 1) HIP_CHECK(hipMalloc(&dbuf, size_t(max_block) * 4));
+  if (rank == 0) {
+    out.assign(size_t(P_.nx * P_.ny), 0.0f);
+    auto place = [&](const Block& b, const float* src) {
+      for (int64_t r = 0; r < b.lx; ++r)
+        std::memcpy(&out[size_t((b.ox + r) * P_.ny + b.oy)], src + r * b.ly, size_t(b.ly) * 4);
+    };
+    place(blk_, mine.data());
+    std::vector<float> tmp(static_cast<size_t>(max_block));
+    for (int r = 1; r < world; ++r) {
+      Block b = make_block(cart_, r, P_.nx, P_.ny);
+      const size_t bytes = size_t(b.lx * b.ly) * 4;
+      if (dev) {
+        Msg m{r, nullptr, 0, dbuf, bytes};
+        tr_->sendrecv(&m, 1, s_comp_);
+        HIP_CHECK(hipMemcpyAsync(tmp.data(), dbuf, bytes, hipMemcpyDeviceToHost, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+      } else {
+        Msg m{r, nullptr, 0, tmp.data(), bytes};
+        tr_->sendrecv(&m, 1, nullptr);
+      }
+      place(b, tmp.data());
+    }
+  } else {
+    const size_t bytes = mine.size() * 4;
+    if (dev) {
+      HIP_CHECK(hipMemcpyAsync(dbuf, mine.data(), bytes, hipMemcpyHostToDevice, s_comp_));
+      Msg m{0, dbuf, bytes, nullptr, 0};
+      tr_->sendrecv(&m, 1, s_comp_);
+      HIP_CHECK(hipStreamSynchronize(s_comp_));
+    } else {
+      Msg m{0, mine.data(), bytes, nullptr, 0};
+      tr_->sendrecv(&m, 1, nullptr);
+    }
+  }
+  if (dbuf) HIP_CHECK(hipFree(dbuf));
+  return out;
+}
+
+void Solver::reduce_scalars(double* f64, int nf, uint64_t* u64, int nu, float* fmax, int nm) {
+  if (tr_->world() == 1) return;
+  if (!tr_->device_memory()) {
+    if (nf) tr_->allreduce_sum_f64(f64, nf, nullptr);
+    if (nu) tr_->allreduce_sum_u64(u64, nu, nullptr);
+    if (nm) tr_->allreduce_max(fmax, nm, nullptr);
+    return;
+  }
+  char* d = static_cast<char*>(d_scratch_);
+  HIP_CHECK(hipMemcpyAsync(d, f64, size_t(nf) * 8, hipMemcpyHostToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(d + 1024, u64, size_t(nu) * 8, hipMemcpyHostToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(d + 2048, fmax, size_t(nm) * 4, hipMemcpyHostToDevice, s_comp_));
+  if (nf) tr_->allreduce_sum_f64(reinterpret_cast<double*>(d), nf, s_comp_);
+  if (nu) tr_->allreduce_sum_u64(reinterpret_cast<uint64_t*>(d + 1024), nu, s_comp_);
+  if (nm) tr_->allreduce_max(reinterpret_cast<float*>(d + 2048), nm, s_comp_);
+  HIP_CHECK(hipMemcpyAsync(f64, d, size_t(nf) * 8, hipMemcpyDeviceToHost, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(u64, d + 1024, size_t(nu) * 8, hipMemcpyDeviceToHost, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(fmax, d + 2048, size_t(nm) * 4, hipMemcpyDeviceToHost, s_comp_));
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+}
+
+Checksum Solver::checksum() {
+  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+  copy_owned(mine.data(), blk_.ly);
+  Checksum c = checksum_block(mine.data(), blk_.ly, blk_.ox, blk_.oy, blk_.lx, blk_.ly, P_.ny);
+  double f[1] = {c.sum};
+  uint64_t u[2] = {c.hash, uint64_t(c.count)};
+  float m[2] = {float(c.max), float(-c.min)};
+  reduce_scalars(f, 1, u, 2, m, 2);
+  Checksum g;
+  g.sum = f[0];
+  g.hash = u[0];
+  g.count = int64_t(u[1]);
+  g.max = m[0];
+  g.min = -m[1];
+  return g;
+}
+
+void Solver::write_bin(const std::string& path) {
+  if (tr_->rank() == 0) {
+    BinHeader h{};
+    std::memcpy(h.magic, "HEATF32", 8);
+    h.version = 1;
+    h.parity = uint32_t(cur_);
+    h.nx = P_.nx;
+    h.ny = P_.ny;
+    h.step = step_;
+    h.cx = P_.cx;
+    h.cy = P_.cy;
+    bin_create(path, h);
+  }
+  tr_->barrier();
+  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+  copy_owned(mine.data(), blk_.ly);
+  bin_write_block(path, P_.nx, P_.ny, blk_.ox, blk_.oy, blk_.lx, blk_.ly, mine.data(), blk_.ly);
+  tr_->barrier();
+}
+
+void Solver::read_bin(const std::string& path) {
+  BinHeader h = bin_read_header(path);
+  HEAT_CHECK(h.nx == P_.nx && h.ny == P_.ny, "checkpoint is %lldx%lld, run is %lldx%lld",
+             (long long)h.nx, (long long)h.ny, (long long)P_.nx, (long long)P_.ny);
+  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+  bin_read_block(path, blk_.ox, blk_.oy, blk_.lx, blk_.ly, mine.data(), blk_.ly);
+  load_owned(mine.data(), blk_.ly, h.step);
+}
+
+}  // namespace heat

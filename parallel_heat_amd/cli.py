@@ -1,0 +1,148 @@
+"""``python -m parallel_heat_amd`` — the Python front end of the ``heat`` CLI.
+
+Same flags as the native ``build/heat`` binary.  Multi-rank runs are launched
+with ``python -m torch.distributed.run --nproc-per-node N -m parallel_heat_amd
+...``: GPU ranks talk over the engine's RCCL communicator, CPU ranks over
+torch.distributed (gloo).  Replaces the reference's -D macro builds
+(``cuda/Makefile``, ``mpi/Makefile:12-22``) with run-time flags.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+
+import torch
+
+from . import _native
+from .models.config import HeatConfig
+from .models.heat2d import HeatSolver
+from .parallel import comm as pcomm
+from .utils import io as hio
+from .utils import report
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="python -m parallel_heat_amd",
+                                description="2-D heat diffusion on MI355X (5-point Jacobi)")
+    a = p.add_argument
+    a("--nx", type=int, default=20)
+    a("--ny", type=int, default=20)
+    a("--steps", type=int, default=10000)
+    a("--cx", type=float, default=0.1)
+    a("--cy", type=float, default=0.1)
+    a("--converge", action="store_true")
+    a("--check-interval", type=int, default=20)
+    a("--eps", type=float, default=1e-3)
+    a("--backend", choices=["cpu", "hip"], default=None)
+    a("--threads", type=int, default=0)
+    a("--kernel", choices=["auto", "naive", "tb"], default="auto")
+    a("--tb-depth", type=int, default=0)
+    a("--decomp", choices=["auto", "rows", "1d", "2d"], default="auto")
+    a("--px", type=int, default=0)
+    a("--py", type=int, default=0)
+    a("--init", choices=["ref-wrap", "exact", "ref64", "random", "zero"], default="ref-wrap")
+    a("--seed", type=int, default=0)
+    a("--out", default=None)
+    a("--out-format", choices=["dat", "bin", "checksum"], default="dat")
+    a("--naming", choices=["plain", "mpi", "cuda"], default="plain")
+    a("--dump-initial", action="store_true")
+    a("--compat", choices=["none", "mpi", "cuda"], default=None)
+    a("--no-graph", action="store_true")
+    a("--no-overlap", action="store_true")
+    a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
+    a("--checkpoint", default=None)
+    a("--checkpoint-every", type=int, default=0)
+    a("--resume", default=None)
+    a("--json", action="store_true")
+    return p
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    backend = args.backend or ("hip" if torch.cuda.is_available() else "cpu")
+    compat = args.compat or {"mpi": "mpi", "cuda": "cuda"}.get(args.naming, "none")
+    cfg = HeatConfig(nx=args.nx, ny=args.ny, steps=args.steps, cx=args.cx, cy=args.cy,
+                     converge=args.converge, check_interval=args.check_interval, eps=args.eps,
+                     init=args.init, seed=args.seed, backend=backend, kernel=args.kernel,
+                     tb_depth=args.tb_depth, threads=args.threads, decomp=args.decomp,
+                     px=args.px, py=args.py, use_graph=not args.no_graph,
+                     overlap=not args.no_overlap, compat=compat)
+    info = pcomm.init_distributed("nccl" if backend == "hip" else "gloo")
+    root = info.is_root
+    out = sys.stdout
+    if root and args.naming == "mpi":
+        out.write(report.mpi_banner(info.world, cfg.nx, cfg.ny, cfg.steps, cfg.converge))
+        out.flush()
+    solver = HeatSolver(cfg, transport=args.transport, dist_info=info)
+    if args.resume:
+        solver.load(args.resume)
+
+    small = cfg.nx * cfg.ny <= (1 << 24)
+    if args.naming == "mpi":
+        init_path, final_path = "initial_im.dat", "final_im.dat"
+    elif args.naming == "cuda":
+        init_path, final_path = None, report.cuda_output_name(cfg.nx, cfg.ny, cfg.steps)
+    else:
+        init_path, final_path = "initial.dat", ("final.dat" if small else None)
+    if args.out is not None:
+        final_path = None if args.out == "none" else args.out
+
+    def emit(path):
+        if not path:
+            return
+        if args.out_format == "bin":
+            solver.save(path)
+        elif args.out_format == "checksum":
+            c = solver.checksum()
+            if root:
+                with open(path, "w") as f:
+                    f.write(json.dumps({"nx": cfg.nx, "ny": cfg.ny, "step": solver.step, **c}) + "\n")
+        else:
+            g = solver.gather()
+            if root:
+                hio.write_dat(path, g)
+
+    if args.dump_initial or args.naming == "mpi":
+        emit(init_path)
+    total = cfg.total_steps()
+    todo = total - solver.step
+    acc = dict(steps_done=0, seconds=0.0, passes=0, exchanges=0, checks=0)
+    converged, converged_at, last = False, -1, -1.0
+    while todo > 0:
+        chunk = min(args.checkpoint_every, todo) if args.checkpoint_every > 0 else todo
+        r = solver.run(chunk)
+        for k in acc:
+            acc[k] += getattr(r, k)
+        last = r.last_resid
+        todo -= r.steps_done
+        if args.checkpoint and args.checkpoint_every > 0:
+            solver.save(args.checkpoint)
+        if r.converged:
+            converged, converged_at = True, r.converged_at
+            break
+    emit(final_path)
+    if root:
+        if cfg.converge:
+            out.write(report.convergence_line(args.naming, converged, converged_at, solver.step))
+        out.write(report.elapsed_line(args.naming, acc["seconds"]))
+        if args.json:
+            cells = cfg.nx * cfg.ny * acc["steps_done"]
+            out.write(report.metrics_json(
+                nx=cfg.nx, ny=cfg.ny, steps=total, steps_done=acc["steps_done"],
+                ranks=info.world, backend=backend,
+                decomp=f"{solver.info.px}x{solver.info.py}", tb_depth=solver.info.tb_depth,
+                seconds=acc["seconds"],
+                mcells_per_s=cells / acc["seconds"] / 1e6 if acc["seconds"] > 0 else 0.0,
+                s_per_1000_iters=acc["seconds"] * 1000 / max(1, acc["steps_done"]),
+                converged=converged, converged_at=converged_at, last_resid=last,
+                passes=acc["passes"], exchanges=acc["exchanges"],
+                transport=solver.transport, native=_native.loaded_path()) + "\n")
+        out.flush()
+    solver.barrier()
+    solver.close()
+    return 0
+
+
+if __name__ == "__main__":  # pragma: no cover
+    sys.exit(main())

@@ -1,0 +1,169 @@
+"""Tensor-level access to the native stencil kernels.
+
+These wrap single kernels of ``csrc/kernels/stencil.hip`` for torch tensors
+(device kernels on ROCm tensors, the OpenMP oracle on CPU tensors), so the
+kernels can be tested against plain PyTorch fp32 and composed into custom
+schedules.  Fields use the engine's memory layout (ghost ring + 256-B pitch,
+``heat::Layout``); ``Field`` owns a torch tensor with that layout.
+
+Reference kernels: ``heat`` (``cuda/cuda_heat.cu:140-163``) and the fused
+``heat<threads>`` + ``semi_reduce`` residual (``:32-138``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from .. import _native
+from ..models.config import INIT_MODES
+from ..parallel.topology import layout
+
+Box = Tuple[int, int, int, int]  # (r0, r1, c0, c1) in local coordinates
+
+
+@dataclass
+class Geom:
+    """Global placement of a local field: local (0,0) is global (gx0, gy0)."""
+    nx: int
+    ny: int
+    gx0: int = 0
+    gy0: int = 0
+    cx: float = 0.1
+    cy: float = 0.1
+
+
+class Field:
+    """A local field (owned lx x ly block + `halo`-deep ghost ring) in a torch tensor."""
+
+    def __init__(self, lx: int, ly: int, halo: int = 1, device="cpu", fill: float = 0.0):
+        self.lx, self.ly, self.halo = lx, ly, halo
+        self.pitch, self.rows, self.hx, self.hy = layout(lx, ly, halo)
+        self.data = torch.full((self.rows, self.pitch), fill, dtype=torch.float32,
+                               device=device)
+
+    @property
+    def device(self):
+        return self.data.device
+
+    def ptr(self) -> int:
+        """Address of owned cell (0, 0)."""
+        return self.data.data_ptr() + 4 * (self.hx * self.pitch + self.hy)
+
+    def view(self, r0: int, r1: int, c0: int, c1: int) -> torch.Tensor:
+        """View of local cells [r0,r1) x [c0,c1) (negative = ghost ring)."""
+        return self.data[self.hx + r0:self.hx + r1, self.hy + c0:self.hy + c1]
+
+    def owned(self) -> torch.Tensor:
+        return self.view(0, self.lx, 0, self.ly)
+
+    def set_owned(self, t: torch.Tensor) -> None:
+        self.owned().copy_(t)
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0
+
+
+def _resid_ptr(resid: Optional[torch.Tensor]) -> Optional[int]:
+    if resid is None:
+        return None
+    if resid.dtype != torch.int32 or resid.numel() < 1:
+        raise ValueError("resid must be an int32 tensor (float bits of max|delta|)")
+    return resid.data_ptr()
+
+
+def resid_value(resid: torch.Tensor) -> float:
+    """Decode the float bits an atomic-max residual word holds."""
+    return float(resid[:1].cpu().view(torch.float32).item())
+
+
+def init_field(f: Field, geom: Geom, mode: str = "ref-wrap", seed: int = 0) -> None:
+    """Fill every cell of the field (owned, ghosts, padding) from the initial condition."""
+    m = INIT_MODES[mode]
+    if f.device.type == "cpu":
+        from ..models.reference import init_grid
+        full = init_grid(geom.nx, geom.ny, mode, seed)  # small fields only
+        f.data.zero_()
+        r0, r1 = max(0, geom.gx0 - f.hx), min(geom.nx, geom.gx0 + f.lx + f.hx)
+        c0, c1 = max(0, geom.gy0 - f.hy), min(geom.ny, geom.gy0 + f.pitch - f.hy)
+        f.data[r0 - geom.gx0 + f.hx:r1 - geom.gx0 + f.hx, c0 - geom.gy0 + f.hy:c1 - geom.gy0 + f.hy] = \
+            torch.from_numpy(full[r0:r1, c0:c1])
+        return
+    _native.call("heat_op_init", ctypes.c_void_p(f.ptr()), f.lx, f.ly, f.halo, geom.gx0,
+                 geom.gy0, geom.nx, geom.ny, m, seed, ctypes.c_void_p(_stream()))
+
+
+def naive_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
+               resid: Optional[torch.Tensor] = None) -> None:
+    """One Jacobi step over `box` (default: the owned block)."""
+    r0, r1, c0, c1 = box or (0, src.lx, 0, src.ly)
+    if src.pitch != dst.pitch:
+        raise ValueError("src/dst layouts differ")
+    if src.device.type == "cpu":
+        r = ctypes.c_float()
+        _native.call("heat_cpu_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
+                     src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy,
+                     r0, r1, c0, c1, ctypes.byref(r) if resid is not None else None)
+        if resid is not None:
+            resid.view(torch.float32)[0] = max(resid_value(resid), r.value)
+        return
+    rp = _resid_ptr(resid)
+    _native.call("heat_op_naive_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
+                 src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy,
+                 r0, r1, c0, c1, ctypes.c_void_p(rp) if rp else None,
+                 ctypes.c_void_p(_stream()))
+
+
+def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
+            boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
+            waves_target: int = 0) -> None:
+    """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes."""
+    if src.device.type == "cpu":
+        raise ValueError("tb_step is a GPU kernel")
+    if not _native.lib().heat_tb_supported(depth):
+        raise ValueError(f"unsupported depth {depth}")
+    if src.halo < depth or src.hy < -(-depth // 4) * 4:
+        raise ValueError("ghost ring thinner than depth")
+    boxes = list(boxes or [(0, src.lx, 0, src.ly)])
+    arr = (ctypes.c_int64 * (4 * len(boxes)))(*[v for b in boxes for v in b])
+    rp = _resid_ptr(resid)
+    _native.call("heat_op_tb_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
+                 src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy, arr,
+                 len(boxes), depth, ctypes.c_void_p(rp) if rp else None,
+                 ctypes.c_void_p(_stream()), waves_target)
+
+
+def pack(f: Field, box: Box, out: torch.Tensor) -> None:
+    r0, r1, c0, c1 = box
+    if f.device.type == "cpu":
+        out.view(r1 - r0, c1 - c0).copy_(f.view(r0, r1, c0, c1))
+        return
+    _native.call("heat_op_pack", ctypes.c_void_p(f.ptr()), f.pitch, r0, r1, c0, c1,
+                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(_stream()))
+
+
+def unpack(buf: torch.Tensor, f: Field, box: Box) -> None:
+    r0, r1, c0, c1 = box
+    if f.device.type == "cpu":
+        f.view(r0, r1, c0, c1).copy_(buf.view(r1 - r0, c1 - c0))
+        return
+    _native.call("heat_op_unpack", ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(f.ptr()),
+                 f.pitch, r0, r1, c0, c1, ctypes.c_void_p(_stream()))
+
+
+def residual(a: Field, b: Field, box: Optional[Box] = None,
+             resid: Optional[torch.Tensor] = None) -> float:
+    """max |a - b| over `box` (owned block by default)."""
+    r0, r1, c0, c1 = box or (0, a.lx, 0, a.ly)
+    if a.device.type == "cpu":
+        return float((a.view(r0, r1, c0, c1) - b.view(r0, r1, c0, c1)).abs().max())
+    own = resid is None
+    if own:
+        resid = torch.zeros(1, dtype=torch.int32, device=a.device)
+    _native.call("heat_op_residual", ctypes.c_void_p(a.ptr()), ctypes.c_void_p(b.ptr()),
+                 a.pitch, r0, r1, c0, c1, ctypes.c_void_p(resid.data_ptr()),
+                 ctypes.c_void_p(_stream()))
+    return resid_value(resid) if own else float("nan")
