@@ -28,7 +28,10 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp $(HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(BUILD)/obj/%.o: csrc/kernels/%.hip $(HDRS)
+KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
+$(BUILD)/obj/tb_scalar.o: HIPFLAGS += -fno-slp-vectorize
+
+$(BUILD)/obj/%.o: csrc/kernels/%.hip $(HDRS) $(KHDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -118,7 +118,8 @@ int heat_op_naive_step(const float* src, float* dst, int64_t pitch, int64_t gx0,
                        int64_t c0, int64_t c1, unsigned* resid, void* stream);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
-                    int nbox, int depth, unsigned* resid, void* stream, int waves_target);
+                    int nbox, int depth, unsigned* resid, void* stream, int waves_target,
+                    int variant /* -1 default; bit0 lag-2, bit1 scalar build */);
 int heat_op_init(float* origin, int64_t lx, int64_t ly, int halo, int64_t gx0, int64_t gy0,
                  int64_t nx, int64_t ny, int mode, uint64_t seed, void* stream);
 int heat_op_pack(const float* origin, int64_t pitch, int64_t r0, int64_t r1, int64_t c0,

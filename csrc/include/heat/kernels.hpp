@@ -52,9 +52,19 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 // [r0-depth, r1+depth) and columns [c0-round_up(depth,4), ...) of src, so the
 // ghost ring must be at least that deep and valid (halo exchanged).
 // Box column starts must be multiples of 4.  `waves_target` steers the row
-// chunking (parallelism vs. redundant halo work).
+// chunking (parallelism vs. redundant halo work): > 0 absolute wave count,
+// 0 default rounds, < 0 that many whole rounds of resident waves.
+// `variant`: bits 0-1 pipeline (0: 3-row rings, skew 1; 1: 4-row rings,
+// skew 2; 2: 2-row rings + copy), bit 2 scalar-update build; -1 = default
+// (HEAT_TB_VARIANT or the tuned choice).
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target = 0);
+             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
+int tb_default_variant();
+int tb_variant_lag(int variant);
+// Default whole-rounds of resident waves per launch (HEAT_TB_ROUNDS, default 1).
+int tb_default_rounds();
+// Resident waves of the TB kernel instantiation on the current device.
+int tb_resident_waves(int depth, int variant);
 
 // Copy a box of a strided field to/from a contiguous buffer (E/W halos).
 void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hipStream_t st);

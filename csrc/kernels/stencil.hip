@@ -19,16 +19,23 @@
 //    results are bitwise equal across kernels, depths and decompositions.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "heat/common.hpp"
 #include "heat/init_fn.hpp"
 #include "heat/kernels.hpp"
+#include "tb_common.hpp"
 
 namespace heat::gpu {
 namespace {
 
-constexpr int kWave = 64;
-
-__device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
+using tbdetail::in_interior;
+using tbdetail::TbArgs;
+using tbdetail::TbBox;
+using tbdetail::wave_max_atomic;
 
 // --------------------------------------------------------------------------
 // init
@@ -47,12 +54,6 @@ __global__ void init_kernel(float* base, int64_t pitch, int64_t rows, int64_t hx
 // --------------------------------------------------------------------------
 // naive: one cell per thread (independent oracle for the TB kernel)
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void wave_max_atomic(unsigned m, unsigned* resid) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) m = max(m, unsigned(__shfl_xor(int(m), off)));
-  if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(resid, m);
-}
-
 __global__ __launch_bounds__(256) void naive_kernel(const float* __restrict__ src,
                                                     float* __restrict__ dst, StencilGeom g,
                                                     Box box, unsigned* resid) {
@@ -69,170 +70,6 @@ __global__ __launch_bounds__(256) void naive_kernel(const float* __restrict__ sr
     m = __float_as_uint(fabsf(out - v));
   }
   if (resid) wave_max_atomic(m, resid);
-}
-
-// --------------------------------------------------------------------------
-// temporally blocked register-streaming kernel
-// --------------------------------------------------------------------------
-struct TbBox {
-  int64_t r0, r1, c0, c1;
-  int nstrips, nchunks, chunk_len, wave_begin;
-};
-
-struct TbArgs {
-  const float* src;
-  float* dst;
-  unsigned* resid;
-  StencilGeom g;
-  int nbox, total_waves;
-  TbBox box[5];
-};
-
-__device__ __forceinline__ float dpp_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
-
-template <bool EDGE>
-struct RowUpdate {
-  float cx, cy;
-  bool cm0, cm1, cm2, cm3;  // per-column "updatable" masks (EDGE only)
-  __device__ __forceinline__ float4 operator()(const float4& a, const float4& b, const float4& c,
-                                               bool row_ok) const {
-    if (EDGE && !row_ok) return b;
-    const float w = dpp_from_left(b.w);
-    const float e = dpp_from_right(b.x);
-    float4 r;
-    r.x = stencil(b.x, a.x, c.x, w, b.y, cx, cy);
-    r.y = stencil(b.y, a.y, c.y, b.x, b.z, cx, cy);
-    r.z = stencil(b.z, a.z, c.z, b.y, b.w, cx, cy);
-    r.w = stencil(b.w, a.w, c.w, b.z, e, cx, cy);
-    if (EDGE) {
-      r.x = cm0 ? r.x : b.x;
-      r.y = cm1 ? r.y : b.y;
-      r.z = cm2 ? r.z : b.z;
-      r.w = cm3 ? r.w : b.w;
-    }
-    return r;
-  }
-};
-
-constexpr int mod3(int v) { return ((v % 3) + 3) % 3; }
-
-template <int K, bool EDGE>
-struct TbStream {
-  // R[s][slot]: level-s rows in a 3-slot ring (level 0 = input rows).
-  float4 R[K][3];
-  float4 P[3];  // prefetch ring (rows i+3)
-  unsigned m = 0;
-
-  template <int U>
-  __device__ __forceinline__ void body(int64_t i, const float* __restrict__ src,
-                                       float* __restrict__ dst, int64_t pitch, int64_t last_in,
-                                       int64_t rb, int64_t re, int64_t gx0, int64_t nx,
-                                       bool store_lane, const RowUpdate<EDGE>& upd,
-                                       bool want_resid) {
-    R[0][U] = P[U];
-    {
-      const int64_t nxt = min(i + 3, last_in);
-      P[U] = *reinterpret_cast<const float4*>(src + nxt * pitch);
-    }
-#pragma unroll
-    for (int s = 1; s < K; ++s) {
-      const bool ok = !EDGE || in_interior(gx0 + (i - s), nx);
-      R[s][mod3(U - s)] =
-          upd(R[s - 1][mod3(U - s - 1)], R[s - 1][mod3(U - s)], R[s - 1][mod3(U - s + 1)], ok);
-    }
-    const int64_t ro = i - K;  // output row of this iteration
-    const bool ok = !EDGE || in_interior(gx0 + ro, nx);
-    const float4& b = R[K - 1][mod3(U - K)];
-    const float4 out = upd(R[K - 1][mod3(U - K - 1)], b, R[K - 1][mod3(U - K + 1)], ok);
-    if (ro >= rb && ro < re && store_lane) {
-      *reinterpret_cast<float4*>(dst + ro * pitch) = out;
-      if (want_resid) {
-        m = max(m, __float_as_uint(fabsf(out.x - b.x)));
-        m = max(m, __float_as_uint(fabsf(out.y - b.y)));
-        m = max(m, __float_as_uint(fabsf(out.z - b.z)));
-        m = max(m, __float_as_uint(fabsf(out.w - b.w)));
-      }
-    }
-  }
-
-  __device__ __forceinline__ void run(const float* __restrict__ src, float* __restrict__ dst,
-                                      int64_t pitch, int64_t rb, int64_t re, int64_t gx0,
-                                      int64_t nx, bool store_lane, const RowUpdate<EDGE>& upd,
-                                      bool want_resid) {
-    // src/dst already offset to this lane's column; rows are absolute local rows.
-    const int64_t first_in = rb - K, last_in = re + K - 1;
-    const int64_t T = last_in - first_in + 1;
-#pragma unroll
-    for (int s = 0; s < K; ++s)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) R[s][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      P[j] = *reinterpret_cast<const float4*>(src + min(first_in + j, last_in) * pitch);
-    for (int64_t t = 0; t < T; t += 3) {
-      const int64_t i = first_in + t;
-      body<0>(i, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-      body<1>(i + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-      body<2>(i + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-    }
-  }
-};
-
-template <int K>
-__global__ __launch_bounds__(256) void tb_kernel(TbArgs a) {
-  constexpr int KK = (K + 3) & ~3;
-  constexpr int W = 256 - 2 * KK;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave >= a.total_waves) return;
-  int bi = 0;
-#pragma unroll
-  for (int j = 1; j < 5; ++j)
-    if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
-  const TbBox bx = a.box[bi];
-  const int w = wave - bx.wave_begin;
-  const int strip = w % bx.nstrips, chunk = w / bx.nstrips;
-  const int64_t cbase = bx.c0 + int64_t(strip) * W;
-  const int64_t cend = min(cbase + W, bx.c1);
-  const int64_t col = cbase - KK + 4 * lane;
-  const bool store_lane = col >= cbase && col < cend;
-  const int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
-  const int64_t re = min(rb + bx.chunk_len, bx.r1);
-
-  const StencilGeom& g = a.g;
-  const float* src = a.src + col;
-  float* dst = a.dst + col;
-  const bool want_resid = a.resid != nullptr;
-
-  // Wave-uniform fast path: every row and column the wave touches is a
-  // global interior cell, so no Dirichlet masking is needed.
-  const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
-  const int64_t gx_lo = g.gx0 + rb - K, gx_hi = g.gx0 + re + K - 1;
-  const bool interior = gy_lo >= 1 && gy_hi <= g.ny - 2 && gx_lo >= 1 && gx_hi <= g.nx - 2;
-  unsigned m;
-  if (interior) {
-    RowUpdate<false> upd{g.cx, g.cy, true, true, true, true};
-    TbStream<K, false> st;
-    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
-    m = st.m;
-  } else {
-    const int64_t gy = g.gy0 + col;
-    RowUpdate<true> upd{g.cx,
-                        g.cy,
-                        in_interior(gy, g.ny),
-                        in_interior(gy + 1, g.ny),
-                        in_interior(gy + 2, g.ny),
-                        in_interior(gy + 3, g.ny)};
-    TbStream<K, true> st;
-    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
-    m = st.m;
-  }
-  if (want_resid) wave_max_atomic(m, a.resid);
 }
 
 // --------------------------------------------------------------------------
@@ -271,12 +108,6 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
 
 int grid_1d(int64_t n) { return int(std::min<int64_t>(ceil_div(n, 256), 256 * 16)); }
 
-template <int K>
-void launch_tb(TbArgs& args, hipStream_t st) {
-  const int blocks = int(ceil_div(args.total_waves, 4));
-  hipLaunchKernelGGL(tb_kernel<K>, dim3(blocks), dim3(256), 0, st, args);
-}
-
 }  // namespace
 
 bool tb_depth_supported(int k) {
@@ -284,6 +115,49 @@ bool tb_depth_supported(int k) {
 }
 
 int tb_strip_width(int k) { return 256 - 2 * int(round_up(k, 4)); }
+
+int tb_variant_lag(int variant) {
+  switch (variant & 3) {
+    case 1: return 2;
+    case 2: return 0;
+    default: return 1;
+  }
+}
+
+int tb_default_rounds() {
+  static const int r = [] {
+    const char* e = std::getenv("HEAT_TB_ROUNDS");
+    return e && *e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  return r;
+}
+
+int tb_resident_waves(int depth, int variant) {
+  // Cached per (device, depth, variant): CUs x resident blocks per CU x 4 waves.
+  static std::map<std::tuple<int, int, int>, int> cache;
+  static std::mutex mu;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_tuple(dev, depth, variant);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int lag = tb_variant_lag(variant);
+  const int per_cu = (variant & 4) ? tbs::occupancy(depth, lag) : tbp::occupancy(depth, lag);
+  const int w = std::max(1, cus * std::max(1, per_cu) * 4);
+  cache.emplace(key, w);
+  return w;
+}
+
+int tb_default_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("HEAT_TB_VARIANT");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 void init_field(float* origin, const Layout& L, int64_t gx0, int64_t gy0, int64_t nx, int64_t ny,
                 int mode, uint64_t seed, hipStream_t st) {
@@ -303,10 +177,17 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 }
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target) {
+             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);
-  if (waves_target <= 0) waves_target = 2048;
+  if (variant < 0) variant = tb_default_variant();
+  const int lag = tb_variant_lag(variant);
+  if (waves_target <= 0) {
+    // Whole rounds of the resident wave capacity: a partial last round leaves
+    // SIMDs idle for the tail of the launch.
+    const int rounds = waves_target < 0 ? -waves_target : tb_default_rounds();
+    waves_target = rounds * tb_resident_waves(depth, variant);
+  }
   const int W = tb_strip_width(depth);
   TbArgs args{};
   args.src = src;
@@ -340,20 +221,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   if (n == 0) return;
   args.nbox = n;
   args.total_waves = waves;
-  switch (depth) {
-    case 1: launch_tb<1>(args, st); break;
-    case 2: launch_tb<2>(args, st); break;
-    case 3: launch_tb<3>(args, st); break;
-    case 4: launch_tb<4>(args, st); break;
-    case 5: launch_tb<5>(args, st); break;
-    case 6: launch_tb<6>(args, st); break;
-    case 7: launch_tb<7>(args, st); break;
-    case 8: launch_tb<8>(args, st); break;
-    case 10: launch_tb<10>(args, st); break;
-    case 12: launch_tb<12>(args, st); break;
-    case 16: launch_tb<16>(args, st); break;
-    default: HEAT_CHECK(false, "unsupported TB depth %d", depth);
-  }
+  const bool ok = (variant & 4) ? tbs::launch(args, depth, lag, st) : tbp::launch(args, depth, lag, st);
+  HEAT_CHECK(ok, "unsupported TB depth %d", depth);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -381,3 +250,8 @@ void residual_box(const float* a, const float* b, int64_t pitch, const Box& box,
 }
 
 }  // namespace heat::gpu
+
+// The packed-update build of the temporally blocked kernel.
+#define HEAT_TB_NS tbp
+#define HEAT_TB_PACKED 1
+#include "tb_stream.inl"

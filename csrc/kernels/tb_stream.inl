@@ -1,0 +1,359 @@
+// Register-streaming temporally blocked Jacobi kernel (the hot kernel).
+//
+// Included by stencil.hip (namespace heat::gpu::tbp, explicit packed-fp32
+// row update) and tb_scalar.hip (namespace heat::gpu::tbs, compiled with
+// -fno-slp-vectorize: scalar row update).  The two builds exist so the row
+// update's instruction selection can be A/B-timed in one process.
+//
+// Structure (one wave = one 256-column strip x one chunk of rows):
+//   lane l holds columns [4l, 4l+4) of the strip as a float4;
+//   level 0 = the input rows, level s = the field after s steps;
+//   every loop iteration loads one input row and advances every level by one
+//   row, keeping each level's last rows in a register ring;
+//   east/west neighbours cross lanes with DPP wave_shr:1 / wave_shl:1.
+// LAG selects the pipeline skew: level s works on row i - LAG*s (LAG 0 is the
+// 2-slot ring below, skew 1).
+//   LAG 1: 3-row rings; the K levels of one iteration form one dependency
+//          chain (level s consumes the row level s-1 produced this iteration).
+//   LAG 2: 4-row rings; level s consumes only rows produced in earlier
+//          iterations, so the K updates of an iteration are independent
+//          (K-way instruction-level parallelism) at the cost of 4/3 the
+//          ring registers and K more pipeline-fill iterations.
+#ifndef HEAT_TB_NS
+#error "define HEAT_TB_NS"
+#endif
+
+namespace heat::gpu::HEAT_TB_NS {
+
+using heat::gpu::tbdetail::TbArgs;
+using heat::gpu::tbdetail::TbBox;
+using heat::gpu::tbdetail::in_interior;
+using heat::gpu::tbdetail::wave_max_atomic;
+
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+template <bool EDGE>
+struct RowUpdate {
+  float cx, cy;
+  bool cm0, cm1, cm2, cm3;  // per-column "updatable" masks (EDGE only)
+  __device__ __forceinline__ float4 operator()(const float4& a, const float4& b, const float4& c,
+                                               bool row_ok) const {
+    if (EDGE && !row_ok) return b;
+    const float w = dpp_from_left(b.w);
+    const float e = dpp_from_right(b.x);
+    float4 r;
+#if HEAT_TB_PACKED
+    // Explicit pairs (x,y) and (z,w): v_pk_add_f32 / v_pk_fma_f32 on aligned
+    // register pairs; the east+west sums are scalar adds (two of them fuse
+    // the DPP lane shift) written straight into aligned pairs.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 m2 = {-2.0f, -2.0f}, cx2 = {cx, cx}, cy2 = {cy, cy};
+    const f2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+    const f2 ns01 = f2{c.x, c.y} + f2{a.x, a.y};
+    const f2 ns23 = f2{c.z, c.w} + f2{a.z, a.w};
+    const f2 ew01 = {b.y + w, b.z + b.x};
+    const f2 ew23 = {b.w + b.y, e + b.z};
+    const f2 tx01 = __builtin_elementwise_fma(m2, b01, ns01);
+    const f2 tx23 = __builtin_elementwise_fma(m2, b23, ns23);
+    const f2 ty01 = __builtin_elementwise_fma(m2, b01, ew01);
+    const f2 ty23 = __builtin_elementwise_fma(m2, b23, ew23);
+    const f2 r01 = __builtin_elementwise_fma(cy2, ty01, __builtin_elementwise_fma(cx2, tx01, b01));
+    const f2 r23 = __builtin_elementwise_fma(cy2, ty23, __builtin_elementwise_fma(cx2, tx23, b23));
+    r = make_float4(r01.x, r01.y, r23.x, r23.y);
+#else
+    r.x = stencil(b.x, a.x, c.x, w, b.y, cx, cy);
+    r.y = stencil(b.y, a.y, c.y, b.x, b.z, cx, cy);
+    r.z = stencil(b.z, a.z, c.z, b.y, b.w, cx, cy);
+    r.w = stencil(b.w, a.w, c.w, b.z, e, cx, cy);
+#endif
+    if (EDGE) {
+      r.x = cm0 ? r.x : b.x;
+      r.y = cm1 ? r.y : b.y;
+      r.z = cm2 ? r.z : b.z;
+      r.w = cm3 ? r.w : b.w;
+    }
+    return r;
+  }
+};
+
+template <int N>
+__device__ constexpr int modn(int v) {
+  return ((v % N) + N) % N;
+}
+
+template <int K, int LAG, bool EDGE>
+struct TbStream {
+  static constexpr int RING = LAG == 0 ? 2 : (LAG == 1 ? 3 : 4);
+  static constexpr int SKEW = LAG == 0 ? 1 : LAG;
+  float4 R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
+  float4 P[RING];     // prefetch ring (input row i + RING)
+  unsigned m = 0;
+
+  __device__ __forceinline__ void emit(const float4& out, const float4& b, int64_t ro,
+                                       float* __restrict__ dst, int64_t pitch, int64_t rb,
+                                       int64_t re, bool store_lane, bool want_resid) {
+    if (ro >= rb && ro < re && store_lane) {
+      *reinterpret_cast<float4*>(dst + ro * pitch) = out;
+      if (want_resid) {
+        m = max(m, __float_as_uint(fabsf(out.x - b.x)));
+        m = max(m, __float_as_uint(fabsf(out.y - b.y)));
+        m = max(m, __float_as_uint(fabsf(out.z - b.z)));
+        m = max(m, __float_as_uint(fabsf(out.w - b.w)));
+      }
+    }
+  }
+
+  template <int U>
+  __device__ __forceinline__ void body(int64_t i, const float* __restrict__ src,
+                                       float* __restrict__ dst, int64_t pitch, int64_t last_in,
+                                       int64_t rb, int64_t re, int64_t gx0, int64_t nx,
+                                       bool store_lane, const RowUpdate<EDGE>& upd,
+                                       bool want_resid) {
+    if constexpr (LAG == 0) {
+      // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
+      // s holds rows i-s-2 (slot (U-s)&1) and i-s-1 (slot (U-s-1)&1).
+      float4 c = P[U];
+      {
+        const int64_t nxt = min(i + RING, last_in);
+        P[U] = *reinterpret_cast<const float4*>(src + nxt * pitch);
+      }
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int sa = modn<2>(U - s), sb = modn<2>(U - s - 1);
+        const int64_t row = i - s - 1;  // row of level s+1 computed now
+        const bool ok = !EDGE || in_interior(gx0 + row, nx);
+        const float4 cn = upd(R[s][sa], R[s][sb], c, ok);
+        if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane, want_resid);
+        R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
+        c = cn;
+      }
+    } else {
+      R[0][U] = P[U];
+      {
+        const int64_t nxt = min(i + RING, last_in);
+        P[U] = *reinterpret_cast<const float4*>(src + nxt * pitch);
+      }
+      // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
+      // iterations, so the order below carries no dependency.
+#pragma unroll
+      for (int s = 1; s < K; ++s) {
+        const int rs = LAG * s;  // this level's row is i - rs
+        const bool ok = !EDGE || in_interior(gx0 + (i - rs), nx);
+        R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
+                                       R[s - 1][modn<RING>(U - rs)],
+                                       R[s - 1][modn<RING>(U - rs + 1)], ok);
+      }
+      const int rK = LAG * K;
+      const int64_t ro = i - rK;  // output row of this iteration
+      const bool ok = !EDGE || in_interior(gx0 + ro, nx);
+      const float4& b = R[K - 1][modn<RING>(U - rK)];
+      const float4 out =
+          upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
+      emit(out, b, ro, dst, pitch, rb, re, store_lane, want_resid);
+    }
+  }
+
+  __device__ __forceinline__ void run(const float* __restrict__ src, float* __restrict__ dst,
+                                      int64_t pitch, int64_t rb, int64_t re, int64_t gx0,
+                                      int64_t nx, bool store_lane, const RowUpdate<EDGE>& upd,
+                                      bool want_resid) {
+    // src/dst are offset to this lane's column; rows are local rows.
+    const int64_t first_in = rb - K, last_in = re + K - 1;
+    // The last output row (re-1) leaves the pipeline at iteration re-1+SKEW*K.
+    const int64_t T = (re - 1 + SKEW * K) - first_in + 1;
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+      for (int j = 0; j < RING; ++j) R[s][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < RING; ++j)
+      P[j] = *reinterpret_cast<const float4*>(src + min(first_in + j, last_in) * pitch);
+    for (int64_t t = 0; t < T; t += RING) {
+      const int64_t i = first_in + t;
+      body<0>(i, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      body<1>(i + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      if constexpr (RING >= 3)
+        body<2>(i + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      if constexpr (RING == 4)
+        body<3>(i + 3, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+    }
+  }
+};
+
+template <int K, int LAG>
+__global__ __launch_bounds__(256) void tb_kernel(TbArgs a) {
+  constexpr int KK = (K + 3) & ~3;
+  constexpr int W = 256 - 2 * KK;
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave >= a.total_waves) return;
+  int bi = 0;
+#pragma unroll
+  for (int j = 1; j < 5; ++j)
+    if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
+  const TbBox bx = a.box[bi];
+  const int w = wave - bx.wave_begin;
+  const int strip = w % bx.nstrips, chunk = w / bx.nstrips;
+  const int64_t cbase = bx.c0 + int64_t(strip) * W;
+  const int64_t cend = min(cbase + W, bx.c1);
+  const int64_t col = cbase - KK + 4 * lane;
+  const bool store_lane = col >= cbase && col < cend;
+  const int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
+  const int64_t re = min(rb + bx.chunk_len, bx.r1);
+
+  const StencilGeom& g = a.g;
+  const float* src = a.src + col;
+  float* dst = a.dst + col;
+  const bool want_resid = a.resid != nullptr;
+
+  // Wave-uniform fast path: every row and column the wave touches is a
+  // global interior cell, so no Dirichlet masking is needed.
+  const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
+  const int64_t gx_lo = g.gx0 + rb - K, gx_hi = g.gx0 + re + K - 1;
+  const bool interior = gy_lo >= 1 && gy_hi <= g.ny - 2 && gx_lo >= 1 && gx_hi <= g.nx - 2;
+  unsigned m;
+  if (interior) {
+    RowUpdate<false> upd{g.cx, g.cy, true, true, true, true};
+    TbStream<K, LAG, false> st;
+    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
+    m = st.m;
+  } else {
+    const int64_t gy = g.gy0 + col;
+    RowUpdate<true> upd{g.cx,
+                        g.cy,
+                        in_interior(gy, g.ny),
+                        in_interior(gy + 1, g.ny),
+                        in_interior(gy + 2, g.ny),
+                        in_interior(gy + 3, g.ny)};
+    TbStream<K, LAG, true> st;
+    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
+    m = st.m;
+  }
+  if (want_resid) wave_max_atomic(m, a.resid);
+}
+
+template <int K, int LAG>
+void launch_k(const TbArgs& args, hipStream_t st) {
+  const int blocks = int((args.total_waves + 3) / 4);
+  hipLaunchKernelGGL((tb_kernel<K, LAG>), dim3(blocks), dim3(256), 0, st, args);
+}
+
+template <int K, int LAG>
+int occ_k() {
+  // 256-thread blocks put one wave on each SIMD, so blocks/CU = waves/SIMD.
+  // The occupancy API can over-report by one block per CU (MI355X_MICROARCH
+  // "Residency"), so also bound it by the VGPR allocation granule of 8.
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tb_kernel<K, LAG>, 256, 0) != hipSuccess)
+    n = 1;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tb_kernel<K, LAG>)) == hipSuccess &&
+      fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    n = std::min(n, std::min(8, 512 / alloc));
+  }
+  return std::max(1, n);
+}
+
+// Resident 256-thread blocks per CU of the (depth, lag) instantiation.
+int occupancy(int depth, int lag) {
+  if (lag == 0) {
+    switch (depth) {
+      case 1: return occ_k<1, 0>();
+      case 2: return occ_k<2, 0>();
+      case 3: return occ_k<3, 0>();
+      case 4: return occ_k<4, 0>();
+      case 5: return occ_k<5, 0>();
+      case 6: return occ_k<6, 0>();
+      case 7: return occ_k<7, 0>();
+      case 8: return occ_k<8, 0>();
+      case 10: return occ_k<10, 0>();
+      case 12: return occ_k<12, 0>();
+      case 16: return occ_k<16, 0>();
+      default: return 1;
+    }
+  }
+  if (lag == 2) {
+    switch (depth) {
+      case 1: return occ_k<1, 2>();
+      case 2: return occ_k<2, 2>();
+      case 3: return occ_k<3, 2>();
+      case 4: return occ_k<4, 2>();
+      case 5: return occ_k<5, 2>();
+      case 6: return occ_k<6, 2>();
+      case 7: return occ_k<7, 2>();
+      case 8: return occ_k<8, 2>();
+      default: break;
+    }
+  }
+  switch (depth) {
+    case 1: return occ_k<1, 1>();
+    case 2: return occ_k<2, 1>();
+    case 3: return occ_k<3, 1>();
+    case 4: return occ_k<4, 1>();
+    case 5: return occ_k<5, 1>();
+    case 6: return occ_k<6, 1>();
+    case 7: return occ_k<7, 1>();
+    case 8: return occ_k<8, 1>();
+    case 10: return occ_k<10, 1>();
+    case 12: return occ_k<12, 1>();
+    case 16: return occ_k<16, 1>();
+    default: return 1;
+  }
+}
+
+// Returns false if (depth, lag) is not instantiated.
+bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
+  if (lag == 0) {
+    switch (depth) {
+      case 1: launch_k<1, 0>(args, st); return true;
+      case 2: launch_k<2, 0>(args, st); return true;
+      case 3: launch_k<3, 0>(args, st); return true;
+      case 4: launch_k<4, 0>(args, st); return true;
+      case 5: launch_k<5, 0>(args, st); return true;
+      case 6: launch_k<6, 0>(args, st); return true;
+      case 7: launch_k<7, 0>(args, st); return true;
+      case 8: launch_k<8, 0>(args, st); return true;
+      case 10: launch_k<10, 0>(args, st); return true;
+      case 12: launch_k<12, 0>(args, st); return true;
+      case 16: launch_k<16, 0>(args, st); return true;
+      default: return false;
+    }
+  }
+  if (lag == 2) {
+    switch (depth) {
+      case 1: launch_k<1, 2>(args, st); return true;
+      case 2: launch_k<2, 2>(args, st); return true;
+      case 3: launch_k<3, 2>(args, st); return true;
+      case 4: launch_k<4, 2>(args, st); return true;
+      case 5: launch_k<5, 2>(args, st); return true;
+      case 6: launch_k<6, 2>(args, st); return true;
+      case 7: launch_k<7, 2>(args, st); return true;
+      case 8: launch_k<8, 2>(args, st); return true;
+      default: break;  // deeper: LAG 1 (register budget)
+    }
+  }
+  switch (depth) {
+    case 1: launch_k<1, 1>(args, st); return true;
+    case 2: launch_k<2, 1>(args, st); return true;
+    case 3: launch_k<3, 1>(args, st); return true;
+    case 4: launch_k<4, 1>(args, st); return true;
+    case 5: launch_k<5, 1>(args, st); return true;
+    case 6: launch_k<6, 1>(args, st); return true;
+    case 7: launch_k<7, 1>(args, st); return true;
+    case 8: launch_k<8, 1>(args, st); return true;
+    case 10: launch_k<10, 1>(args, st); return true;
+    case 12: launch_k<12, 1>(args, st); return true;
+    case 16: launch_k<16, 1>(args, st); return true;
+    default: return false;
+  }
+}
+
+}  // namespace heat::gpu::HEAT_TB_NS

@@ -119,8 +119,12 @@ def naive_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
 
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
-            waves_target: int = 0) -> None:
-    """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes."""
+            waves_target: int = 0, variant: int = -1) -> None:
+    """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes.
+
+    variant: -1 default; bits 0-1 pipeline (0 ring-3, 1 ring-4 skew-2, 2 ring-2 + copy),
+    bit 2 the scalar build.
+    """
     if src.device.type == "cpu":
         raise ValueError("tb_step is a GPU kernel")
     if not _native.lib().heat_tb_supported(depth):
@@ -133,7 +137,7 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
     _native.call("heat_op_tb_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
                  src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy, arr,
                  len(boxes), depth, ctypes.c_void_p(rp) if rp else None,
-                 ctypes.c_void_p(_stream()), waves_target)
+                 ctypes.c_void_p(_stream()), waves_target, variant)
 
 
 def pack(f: Field, box: Box, out: torch.Tensor) -> None:

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""A/B sweep of the temporally blocked kernel on one GPU (interleaved rounds in
+one process, median of rounds).  Prints Gcells/s per (variant, depth, waves).
+
+    python tools/tb_sweep.py --n 8192 --depths 4,6,8 --variants 0,1,2,3 --waves 1024,2048,4096
+"""
+import argparse
+import itertools
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from parallel_heat_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--depths", default="4,6,8")
+    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--waves", default="2048")
+    ap.add_argument("--iters", type=int, default=200, help="steps per timed sample")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    n = args.n
+    depths = [int(x) for x in args.depths.split(",")]
+    variants = [int(x) for x in args.variants.split(",")]
+    waves = [int(x) for x in args.waves.split(",")]
+    H = max(depths)
+    g = ops.Geom(nx=n, ny=n)
+    a = ops.Field(n, n, H, dev)
+    b = ops.Field(n, n, H, dev)
+    ops.init_field(a, g, "random", 1)
+    ops.init_field(b, g, "random", 1)
+    combos = list(itertools.product(variants, depths, waves))
+    res = {c: [] for c in combos}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for c in combos:  # warm-up / first-launch costs
+        v, k, w = c
+        ops.tb_step(a, b, g, k, waves_target=w, variant=v)
+    torch.cuda.synchronize()
+    for _ in range(args.rounds):
+        for c in combos:
+            v, k, w = c
+            passes = max(1, args.iters // k)
+            src, dst = a, b
+            ev0.record()
+            for _ in range(passes):
+                ops.tb_step(src, dst, g, k, waves_target=w, variant=v)
+                src, dst = dst, src
+            ev1.record()
+            ev1.synchronize()
+            ms = ev0.elapsed_time(ev1)
+            res[c].append(n * n * passes * k / (ms * 1e-3) / 1e9)
+    rows = []
+    for c in combos:
+        v, k, w = c
+        med = statistics.median(res[c])
+        rows.append({"variant": v, "pipe": ["ring3", "ring4", "ring2"][v & 3], "build": "scalar" if v & 4 else "packed",
+                     "depth": k, "waves": w, "gcells_s": round(med, 1),
+                     "min": round(min(res[c]), 1), "max": round(max(res[c]), 1),
+                     "ms_per_1000": round(n * n * 1000 / (med * 1e9) * 1e3, 3)})
+    rows.sort(key=lambda r: -r["gcells_s"])
+    for r in rows:
+        print(json.dumps(r))
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
