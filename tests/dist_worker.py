@@ -1,0 +1,57 @@
+"""Multi-process worker used by the distributed tests (gloo on CPU, or one
+shared GPU with host-staged halos)."""
+import os
+import socket
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parallel_heat_amd import HeatConfig, HeatSolver
+    from parallel_heat_amd.parallel.comm import DistInfo
+
+    cfg = HeatConfig(**cfg_kwargs)
+    s = HeatSolver(cfg, transport=transport, dist_info=DistInfo(rank, world, rank),
+                   device=0 if cfg.backend == "hip" else None)
+    conv, conv_at, done = False, -1, 0
+    for n in (chunks or [steps]):
+        r = s.run(n)
+        done += r.steps_done
+        if r.converged:
+            conv, conv_at = True, r.converged_at
+            break
+    g = s.gather()
+    cs = s.checksum()
+    if rank == 0:
+        np.savez(out_path, grid=g, conv=conv, conv_at=conv_at, done=done, hash=cs["hash"],
+                 px=s.info.px, py=s.info.py, exchanges=r.exchanges)
+    s.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_world(world, cfg_kwargs, steps, tmp_path, transport="torch", chunks=None):
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / f"out_{world}_{os.getpid()}.npz")
+    mp.spawn(worker, args=(world, free_port(), cfg_kwargs, steps, out, transport, chunks),
+             nprocs=world, join=True)
+    return dict(np.load(out))

@@ -1,0 +1,140 @@
+"""The `heat` CLI (native binary) and `python -m parallel_heat_amd`: reference
+output names and lines, multi-process TCP runs, checkpoint/resume."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from parallel_heat_amd import HeatConfig, HeatSolver, _native
+from parallel_heat_amd.utils import io as hio
+
+from .dist_worker import free_port
+
+HEAT = str(_native.CLI_PATH)
+ROOT = str(_native.REPO_DIR)
+
+
+def heat(args, cwd, env=None, check=True):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([HEAT] + args, cwd=cwd, env=e, capture_output=True, text=True,
+                          check=check, timeout=300)
+
+
+def reference_grid(nx, ny, steps, **kw):
+    with HeatSolver(HeatConfig(nx=nx, ny=ny, steps=steps, backend="cpu", **kw)) as s:
+        s.run()
+        return s.gather()
+
+
+def test_cli_mpi_naming_and_lines(tmp_path):
+    p = heat(["--backend", "cpu", "--nx", "20", "--ny", "20", "--steps", "100", "--naming", "mpi"],
+             tmp_path)
+    lines = p.stdout.splitlines()
+    assert lines[0] == "Starting mpi_heat2D with 1 worker tasks."
+    assert lines[1] == "Grid size: X= 20  Y= 20  Time steps= 100"
+    assert lines[2].startswith("Elapsed time ") and lines[2].endswith(" secs")
+    assert (tmp_path / "initial_im.dat").exists()
+    # compat=mpi -> STEPS+1 updates
+    g = reference_grid(20, 20, 100, compat="mpi")
+    ref = tmp_path / "ref.dat"
+    hio.write_dat(str(ref), g)
+    assert (tmp_path / "final_im.dat").read_bytes() == ref.read_bytes()
+
+
+def test_cli_cuda_naming_and_convergence(tmp_path):
+    p = heat(["--backend", "cpu", "--nx", "24", "--ny", "30", "--steps", "10000", "--converge",
+              "--naming", "cuda"], tmp_path)
+    # NB for 24x30 with T=32: ceil(22/32)*ceil(28/32) = 1 block
+    assert (tmp_path / "out_cuda_1024_1_10000.dat").exists()
+    first = p.stdout.splitlines()[0]
+    assert first.startswith("Converged at ") and first.endswith(" steps")
+    k = int(first.split()[2])
+    assert k % 20 == 0  # CUDA prints i with i % CHECK_INTERVAL == 0
+    assert p.stdout.splitlines()[1].startswith("Elapsed time: ")
+
+
+def test_cli_json_and_checksum(tmp_path):
+    p = heat(["--backend", "cpu", "--nx", "64", "--ny", "48", "--steps", "30", "--init", "random",
+              "--out-format", "checksum", "--out", "cs.json", "--json"], tmp_path)
+    m = json.loads(p.stdout.splitlines()[-1])
+    assert m["steps_done"] == 30 and m["backend"] == "cpu" and m["mcells_per_s"] > 0
+    cs = json.loads((tmp_path / "cs.json").read_text())
+    with HeatSolver(HeatConfig(nx=64, ny=48, steps=30, init="random", backend="cpu")) as s:
+        s.run()
+        assert cs["hash"] == s.checksum()["hash"]
+
+
+@pytest.mark.parametrize("world,extra", [(2, []), (4, []), (4, ["--decomp", "rows", "--tb-depth", "3"]),
+                                         (3, ["--px", "1", "--py", "3"])])
+def test_cli_tcp_multiprocess_invariance(tmp_path, world, extra):
+    port = free_port()
+    base = ["--backend", "cpu", "--nx", "41", "--ny", "39", "--steps", "57", "--init", "random",
+            "--seed", "3", "--out", "g.bin", "--out-format", "bin", "--transport", "tcp",
+            "--port", str(port)] + extra
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1")
+        procs.append(subprocess.Popen([HEAT] + base, cwd=tmp_path, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    g, h = hio.read_bin(str(tmp_path / "g.bin"))
+    assert h["step"] == 57
+    ref = reference_grid(41, 39, 57, init="random", seed=3)
+    assert np.array_equal(np.asarray(g), ref)
+
+
+def test_cli_checkpoint_resume(tmp_path):
+    heat(["--backend", "cpu", "--nx", "30", "--ny", "30", "--steps", "40", "--init", "random",
+          "--checkpoint", "ck.bin", "--checkpoint-every", "25", "--out", "full.bin",
+          "--out-format", "bin"], tmp_path)
+    # ck.bin holds the state after the last chunk (40); resume a 25-step checkpoint instead
+    heat(["--backend", "cpu", "--nx", "30", "--ny", "30", "--steps", "25", "--init", "random",
+          "--out", "c25.bin", "--out-format", "bin"], tmp_path)
+    heat(["--backend", "cpu", "--nx", "30", "--ny", "30", "--steps", "40", "--init", "random",
+          "--resume", "c25.bin", "--out", "resumed.bin", "--out-format", "bin"], tmp_path)
+    a, _ = hio.read_bin(str(tmp_path / "full.bin"))
+    b, hb = hio.read_bin(str(tmp_path / "resumed.bin"))
+    c, hc = hio.read_bin(str(tmp_path / "ck.bin"))
+    assert hb["step"] == 40 and hc["step"] == 40
+    assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert np.array_equal(np.asarray(a), np.asarray(c))
+
+
+def test_python_cli(tmp_path):
+    p = subprocess.run([sys.executable, "-m", "parallel_heat_amd", "--backend", "cpu", "--nx", "20",
+                        "--ny", "20", "--steps", "100", "--naming", "mpi", "--json"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.splitlines()
+    assert lines[0] == "Starting mpi_heat2D with 1 worker tasks."
+    m = json.loads(lines[-1])
+    assert m["steps_done"] == 101
+    native = tmp_path / "native"
+    native.mkdir()
+    heat(["--backend", "cpu", "--nx", "20", "--ny", "20", "--steps", "100", "--naming", "mpi"],
+         native)
+    assert (tmp_path / "final_im.dat").read_bytes() == (native / "final_im.dat").read_bytes()
+
+
+def test_python_cli_torchrun_gloo(tmp_path):
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "parallel_heat_amd",
+           "--backend", "cpu", "--nx", "33", "--ny", "21", "--steps", "40", "--init", "random",
+           "--out", "g.dat", "--json"]
+    p = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    m = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert m["ranks"] == 2 and m["transport"] == "torch"
+    g = hio.read_dat(str(tmp_path / "g.dat"))
+    ref = reference_grid(33, 21, 40, init="random")
+    assert np.allclose(g, np.round(ref, 1), atol=0.051)

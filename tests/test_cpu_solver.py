@@ -1,0 +1,126 @@
+"""CPU oracle backend of the native engine vs the NumPy reference, halo-depth
+invariance, convergence schedules (canonical / mpi / cuda compat), checkpoint."""
+import numpy as np
+import pytest
+
+from parallel_heat_amd import HeatConfig, HeatSolver
+from parallel_heat_amd.models import reference as R
+
+
+def run(cfg, steps=None):
+    with HeatSolver(cfg) as s:
+        r = s.run(steps)
+        return s.gather(), r
+
+
+@pytest.mark.parametrize("nx,ny,steps,init", [(20, 20, 100, "ref-wrap"), (256, 256, 100, "ref-wrap"),
+                                              (37, 53, 60, "random"), (3, 9, 10, "random")])
+def test_cpu_matches_numpy(nx, ny, steps, init):
+    cfg = HeatConfig(nx=nx, ny=ny, steps=steps, init=init, seed=4, backend="cpu")
+    g, r = run(cfg)
+    ref, done, _ = R.run_np(nx, ny, steps, init=init, seed=4)
+    assert r.steps_done == steps == done
+    # FMA (engine) vs separately rounded float32 (NumPy): a few ulps.
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert np.abs(g - ref).max() <= 2e-6 * scale
+
+
+def test_boundary_ring_fixed():
+    cfg = HeatConfig(nx=30, ny=40, steps=50, init="random", seed=1, backend="cpu")
+    g, _ = run(cfg)
+    g0 = R.init_grid(30, 40, "random", 1)
+    for sl in (np.s_[0, :], np.s_[-1, :], np.s_[:, 0], np.s_[:, -1]):
+        assert np.array_equal(g[sl], g0[sl])
+
+
+@pytest.mark.parametrize("depth", [2, 3, 5])
+def test_halo_depth_invariance_single_rank(depth):
+    cfg = HeatConfig(nx=41, ny=29, steps=23, init="random", backend="cpu")
+    a, _ = run(cfg)
+    b, _ = run(cfg.replace(tb_depth=depth))
+    assert np.array_equal(a, b)
+
+
+def test_threads_invariance():
+    cfg = HeatConfig(nx=64, ny=80, steps=20, init="random", backend="cpu")
+    a, _ = run(cfg.replace(threads=1))
+    b, _ = run(cfg.replace(threads=4))
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("compat", ["none", "mpi", "cuda"])
+def test_convergence_schedule_matches_reference_semantics(compat):
+    cfg = HeatConfig(nx=24, ny=30, steps=20000, converge=True, check_interval=20, eps=1e-3,
+                     backend="cpu", compat=compat)
+    g, r = run(cfg)
+    ref, done, conv_at = R.run_np(24, 30, 20000, converge=True, check_interval=20, eps=1e-3,
+                                  compat=compat)
+    assert r.converged and conv_at > 0
+    assert r.converged_at == conv_at
+    if compat == "cuda":
+        assert (r.converged_at - 1) % 20 == 0   # checks after steps 1, 21, 41, ...
+    else:
+        assert r.converged_at % 20 == 0
+    assert r.last_resid < 1e-3 or (compat == "mpi" and r.last_resid <= 1e-3)
+
+
+def test_not_converged_runs_all_steps_and_mpi_adds_one():
+    cfg = HeatConfig(nx=40, ny=40, steps=100, converge=True, check_interval=20, backend="cpu")
+    _, r = run(cfg)
+    assert not r.converged and r.steps_done == 100 and r.checks == 5
+    _, r = run(cfg.replace(compat="mpi"))
+    assert r.steps_done == 101  # STEPS+1 iterations
+
+
+def test_run_in_chunks_equals_one_run():
+    cfg = HeatConfig(nx=50, ny=60, steps=0, init="random", backend="cpu", tb_depth=3)
+    with HeatSolver(cfg) as s:
+        for n in (7, 1, 13, 9):
+            s.run(n)
+        a = s.gather()
+    b, _ = run(cfg.replace(tb_depth=1), 30)
+    assert np.array_equal(a, b)
+
+
+def test_checkpoint_resume_cpu(tmp_path):
+    cfg = HeatConfig(nx=33, ny=47, steps=40, init="random", backend="cpu")
+    full, _ = run(cfg)
+    with HeatSolver(cfg) as s:
+        s.run(15)
+        s.save(str(tmp_path / "c.bin"))
+    with HeatSolver(cfg) as s:
+        s.load(str(tmp_path / "c.bin"))
+        assert s.step == 15
+        s.run(25)
+        assert np.array_equal(s.gather(), full)
+
+
+def test_checksum_and_local_views():
+    cfg = HeatConfig(nx=17, ny=19, steps=5, init="random", backend="cpu")
+    with HeatSolver(cfg) as s:
+        s.run()
+        g = s.gather()
+        assert np.array_equal(s.local(), g)
+        c = s.checksum()
+        assert c["count"] == 17 * 19
+        assert abs(c["sum"] - float(g.astype(np.float64).sum())) < 1e-6 * abs(c["sum"]) + 1e-6
+        assert c["max"] == float(g.max()) and c["min"] == float(g.min())
+        s.load_local(np.zeros_like(g), step=0)
+        assert not s.gather().any()
+
+
+def test_nan_detected():
+    cfg = HeatConfig(nx=16, ny=16, steps=100, converge=True, check_interval=5, backend="cpu")
+    with HeatSolver(cfg) as s:
+        g = s.local()
+        g[5, 5] = np.nan
+        s.load_local(g)
+        with pytest.raises(Exception, match="non-finite"):
+            s.run()
+
+
+def test_invalid_config():
+    with pytest.raises(ValueError):
+        HeatConfig(nx=0).validate()
+    with pytest.raises(ValueError):
+        HeatConfig(init="bogus").validate()
