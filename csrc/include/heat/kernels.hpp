@@ -55,7 +55,8 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 // chunking (parallelism vs. redundant halo work): > 0 absolute wave count,
 // 0 default rounds, < 0 that many whole rounds of resident waves.
 // `variant`: bits 0-1 pipeline (0: 3-row rings, skew 1; 1: 4-row rings,
-// skew 2; 2: 2-row rings + copy), bit 2 scalar-update build; -1 = default
+// skew 2; 2: 2-row rings + copy; 3: 3-row rings + ramp skip), bit 2
+// scalar-update build; -1 = default
 // (HEAT_TB_VARIANT or the tuned choice).
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);

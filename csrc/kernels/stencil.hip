@@ -120,6 +120,7 @@ int tb_variant_lag(int variant) {
   switch (variant & 3) {
     case 1: return 2;
     case 2: return 0;
+    case 3: return 3;
     default: return 1;
   }
 }
@@ -154,7 +155,7 @@ int tb_resident_waves(int depth, int variant) {
 int tb_default_variant() {
   static const int v = [] {
     const char* e = std::getenv("HEAT_TB_VARIANT");
-    return e && *e ? std::atoi(e) : 0;
+    return e && *e ? std::atoi(e) : 7;  // ring-3 + ramp skip, scalar build (tools/tb_sweep.py)
   }();
   return v;
 }
@@ -200,7 +201,9 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   int64_t total_strip_rows = 0;
   for (int b = 0; b < nbox; ++b)
     if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
-  const int64_t min_len = std::max<int64_t>(4 * depth, 16);
+  // Minimum chunk length in rows (multiples of depth; HEAT_TB_MINLEN overrides).
+  const char* ml = std::getenv("HEAT_TB_MINLEN");
+  const int64_t min_len = ml && *ml ? std::max(1, std::atoi(ml)) : std::max<int64_t>(depth, 8);
   int64_t len = std::max<int64_t>(min_len, ceil_div(total_strip_rows, waves_target));
   int n = 0, waves = 0;
   for (int b = 0; b < nbox; ++b) {

@@ -88,8 +88,10 @@ __device__ constexpr int modn(int v) {
 
 template <int K, int LAG, bool EDGE>
 struct TbStream {
-  static constexpr int RING = LAG == 0 ? 2 : (LAG == 1 ? 3 : 4);
-  static constexpr int SKEW = LAG == 0 ? 1 : LAG;
+  // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
+  static constexpr int RING = LAG == 0 ? 2 : (LAG == 2 ? 4 : 3);
+  static constexpr int SKEW = LAG == 2 ? 2 : 1;
+  static constexpr int STEP = LAG == 2 ? 2 : 1;  // row skew per level in the ring bodies
   float4 R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
   float4 P[RING];     // prefetch ring (input row i + RING)
   unsigned m = 0;
@@ -109,7 +111,7 @@ struct TbStream {
   }
 
   template <int U>
-  __device__ __forceinline__ void body(int64_t i, const float* __restrict__ src,
+  __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int64_t gx0, int64_t nx,
                                        bool store_lane, const RowUpdate<EDGE>& upd,
@@ -144,19 +146,46 @@ struct TbStream {
       // iterations, so the order below carries no dependency.
 #pragma unroll
       for (int s = 1; s < K; ++s) {
-        const int rs = LAG * s;  // this level's row is i - rs
+        const int rs = STEP * s;  // this level's row is i - rs
         const bool ok = !EDGE || in_interior(gx0 + (i - rs), nx);
         R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
                                        R[s - 1][modn<RING>(U - rs)],
                                        R[s - 1][modn<RING>(U - rs + 1)], ok);
       }
-      const int rK = LAG * K;
+      const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
       const bool ok = !EDGE || in_interior(gx0 + ro, nx);
       const float4& b = R[K - 1][modn<RING>(U - rK)];
       const float4 out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
       emit(out, b, ro, dst, pitch, rb, re, store_lane, want_resid);
+    }
+  }
+
+  template <int T, int S>
+  __device__ __forceinline__ void ramp_levels(int64_t i, int64_t gx0, int64_t nx,
+                                              const RowUpdate<EDGE>& upd) {
+    if constexpr (S < K) {
+      if constexpr (2 * S <= T) {
+        const bool ok = !EDGE || in_interior(gx0 + (i - S), nx);
+        R[S][modn<3>(T - S)] = upd(R[S - 1][modn<3>(T - S - 1)], R[S - 1][modn<3>(T - S)],
+                                   R[S - 1][modn<3>(T - S + 1)], ok);
+      }
+      ramp_levels<T, S + 1>(i, gx0, nx, upd);
+    }
+  }
+  template <int T>
+  __device__ __forceinline__ void ramp(int64_t first_in, const float* __restrict__ src,
+                                       int64_t pitch, int64_t last_in, int64_t gx0, int64_t nx,
+                                       const RowUpdate<EDGE>& upd) {
+    if constexpr (T < 2 * K) {
+      constexpr int U = T % 3;
+      const int64_t i = first_in + T;
+      R[0][U] = P[U];
+      P[U] = *reinterpret_cast<const float4*>(src + min(i + 3, last_in) * pitch);
+      ramp_levels<T, 1>(i, gx0, nx, upd);
+      __builtin_amdgcn_sched_barrier(0);
+      ramp<T + 1>(first_in, src, pitch, last_in, gx0, nx, upd);
     }
   }
 
@@ -175,14 +204,34 @@ struct TbStream {
 #pragma unroll
     for (int j = 0; j < RING; ++j)
       P[j] = *reinterpret_cast<const float4*>(src + min(first_in + j, last_in) * pitch);
+    if constexpr (LAG == 3) {
+      // Pipeline ramp: during iteration t < 2K only levels s <= t/2 compute
+      // rows the chunk's output trapezoid needs; a plain loop would compute
+      // 2s useless rows per level per chunk (a third of all work for short
+      // chunks).  The ramp is unrolled at compile time, one scheduling
+      // region per iteration (keeps register pressure at the loop's level).
+      ramp<0>(first_in, src, pitch, last_in, gx0, nx, upd);
+      constexpr int U0 = (2 * K) % 3;
+      for (int64_t t = 2 * K; t < T; t += 3) {
+        const int64_t i = first_in + t;
+        body<U0>(i, t, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+        body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane,
+                           upd, want_resid);
+        body<(U0 + 2) % 3>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane,
+                           upd, want_resid);
+      }
+      return;
+    }
     for (int64_t t = 0; t < T; t += RING) {
       const int64_t i = first_in + t;
-      body<0>(i, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-      body<1>(i + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      body<0>(i, t, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      body<1>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
       if constexpr (RING >= 3)
-        body<2>(i + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+        body<2>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd,
+                want_resid);
       if constexpr (RING == 4)
-        body<3>(i + 3, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+        body<3>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd,
+                want_resid);
     }
   }
 };
@@ -264,6 +313,22 @@ int occ_k() {
 
 // Resident 256-thread blocks per CU of the (depth, lag) instantiation.
 int occupancy(int depth, int lag) {
+  if (lag == 3) {
+  switch (depth) {
+    case 1: return occ_k<1, 3>();
+    case 2: return occ_k<2, 3>();
+    case 3: return occ_k<3, 3>();
+    case 4: return occ_k<4, 3>();
+    case 5: return occ_k<5, 3>();
+    case 6: return occ_k<6, 3>();
+    case 7: return occ_k<7, 3>();
+    case 8: return occ_k<8, 3>();
+    case 10: return occ_k<10, 3>();
+    case 12: return occ_k<12, 3>();
+    case 16: return occ_k<16, 3>();
+    default: return 1;
+    }
+  }
   if (lag == 0) {
     switch (depth) {
       case 1: return occ_k<1, 0>();
@@ -311,6 +376,22 @@ int occupancy(int depth, int lag) {
 
 // Returns false if (depth, lag) is not instantiated.
 bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
+  if (lag == 3) {
+  switch (depth) {
+    case 1: launch_k<1, 3>(args, st); return true;
+    case 2: launch_k<2, 3>(args, st); return true;
+    case 3: launch_k<3, 3>(args, st); return true;
+    case 4: launch_k<4, 3>(args, st); return true;
+    case 5: launch_k<5, 3>(args, st); return true;
+    case 6: launch_k<6, 3>(args, st); return true;
+    case 7: launch_k<7, 3>(args, st); return true;
+    case 8: launch_k<8, 3>(args, st); return true;
+    case 10: launch_k<10, 3>(args, st); return true;
+    case 12: launch_k<12, 3>(args, st); return true;
+    case 16: launch_k<16, 3>(args, st); return true;
+    default: return false;
+    }
+  }
   if (lag == 0) {
     switch (depth) {
       case 1: launch_k<1, 0>(args, st); return true;

@@ -21,6 +21,7 @@ from parallel_heat_amd import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--nx", type=int, default=0, help="rows (default --n)")
     ap.add_argument("--depths", default="4,6,8")
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--waves", default="2048")
@@ -30,13 +31,14 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = args.n
+    nx = args.nx or n
     depths = [int(x) for x in args.depths.split(",")]
     variants = [int(x) for x in args.variants.split(",")]
     waves = [int(x) for x in args.waves.split(",")]
     H = max(depths)
-    g = ops.Geom(nx=n, ny=n)
-    a = ops.Field(n, n, H, dev)
-    b = ops.Field(n, n, H, dev)
+    g = ops.Geom(nx=nx, ny=n)
+    a = ops.Field(nx, n, H, dev)
+    b = ops.Field(nx, n, H, dev)
     ops.init_field(a, g, "random", 1)
     ops.init_field(b, g, "random", 1)
     combos = list(itertools.product(variants, depths, waves))
@@ -58,15 +60,16 @@ def main():
             ev1.record()
             ev1.synchronize()
             ms = ev0.elapsed_time(ev1)
-            res[c].append(n * n * passes * k / (ms * 1e-3) / 1e9)
+            res[c].append(nx * n * passes * k / (ms * 1e-3) / 1e9)
     rows = []
     for c in combos:
         v, k, w = c
         med = statistics.median(res[c])
-        rows.append({"variant": v, "pipe": ["ring3", "ring4", "ring2"][v & 3], "build": "scalar" if v & 4 else "packed",
+        rows.append({"variant": v, "pipe": ["ring3", "ring4", "ring2", "ring3ramp"][v & 3], "build": "scalar" if v & 4 else "packed",
                      "depth": k, "waves": w, "gcells_s": round(med, 1),
                      "min": round(min(res[c]), 1), "max": round(max(res[c]), 1),
-                     "ms_per_1000": round(n * n * 1000 / (med * 1e9) * 1e3, 3)})
+                     "nx": nx, "ny": n,
+                     "ms_per_1000": round(nx * n * 1000 / (med * 1e9) * 1e3, 3)})
     rows.sort(key=lambda r: -r["gcells_s"])
     for r in rows:
         print(json.dumps(r))
