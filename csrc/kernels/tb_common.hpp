@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "heat/init_fn.hpp"
 #include "heat/kernels.hpp"
 

@@ -37,13 +37,22 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
-template <bool EDGE>
+// Dirichlet handling modes (wave-uniform, chosen per wave in tb_kernel).
+// Cells outside the plate are don't-care (their values only ever flow
+// further out), so only the boundary ring itself must be kept:
+//   MODE 0  interior: no wave cell is on the ring;
+//   MODE 1  left edge strip: global column 0 is element 0 of one lane;
+//   MODE 2+j right edge strip: global column ny-1 is element j of one lane;
+//   MODE 6  generic: per-lane column masks AND the (uniform) row test.
+constexpr int kModeGeneric = 6;
+
+template <int MODE>
 struct RowUpdate {
   float cx, cy;
-  bool cm0, cm1, cm2, cm3;  // per-column "updatable" masks (EDGE only)
+  bool cm0, cm1, cm2, cm3;  // MODE 6: per-column "updatable" masks; MODE 1-5: cm0 = this
+                            // lane holds the boundary column
   __device__ __forceinline__ float4 operator()(const float4& a, const float4& b, const float4& c,
                                                bool row_ok) const {
-    if (EDGE && !row_ok) return b;
     const float w = dpp_from_left(b.w);
     const float e = dpp_from_right(b.x);
     float4 r;
@@ -71,23 +80,40 @@ struct RowUpdate {
     r.z = stencil(b.z, a.z, c.z, b.y, b.w, cx, cy);
     r.w = stencil(b.w, a.w, c.w, b.z, e, cx, cy);
 #endif
-    if (EDGE) {
-      r.x = cm0 ? r.x : b.x;
-      r.y = cm1 ? r.y : b.y;
-      r.z = cm2 ? r.z : b.z;
-      r.w = cm3 ? r.w : b.w;
+    if constexpr (MODE == kModeGeneric) {
+      // Branch-free: keep b where the row (wave-uniform) or the column
+      // (per lane) is not a global interior cell.
+      r.x = (cm0 && row_ok) ? r.x : b.x;
+      r.y = (cm1 && row_ok) ? r.y : b.y;
+      r.z = (cm2 && row_ok) ? r.z : b.z;
+      r.w = (cm3 && row_ok) ? r.w : b.w;
+    } else if constexpr (MODE == 1 || MODE == 2) {
+      r.x = cm0 ? b.x : r.x;  // one v_cndmask per row and level
+    } else if constexpr (MODE == 3) {
+      r.y = cm0 ? b.y : r.y;
+    } else if constexpr (MODE == 4) {
+      r.z = cm0 ? b.z : r.z;
+    } else if constexpr (MODE == 5) {
+      r.w = cm0 ? b.w : r.w;
     }
     return r;
   }
 };
+
+// Local row r is a global interior row iff rlo <= r <= rhi (32-bit, uniform).
+__device__ __forceinline__ bool row_in(int64_t r, int rlo, int rhi) {
+  const int ri = int(r);
+  return ri >= rlo && ri <= rhi;
+}
 
 template <int N>
 __device__ constexpr int modn(int v) {
   return ((v % N) + N) % N;
 }
 
-template <int K, int LAG, bool EDGE>
+template <int K, int LAG, int MODE>
 struct TbStream {
+  static constexpr bool ROWCHK = MODE == kModeGeneric;
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
   static constexpr int RING = LAG == 0 ? 2 : (LAG == 2 ? 4 : 3);
   static constexpr int SKEW = LAG == 2 ? 2 : 1;
@@ -113,8 +139,8 @@ struct TbStream {
   template <int U>
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
-                                       int64_t rb, int64_t re, int64_t gx0, int64_t nx,
-                                       bool store_lane, const RowUpdate<EDGE>& upd,
+                                       int64_t rb, int64_t re, int rlo, int rhi,
+                                       bool store_lane, const RowUpdate<MODE>& upd,
                                        bool want_resid) {
     if constexpr (LAG == 0) {
       // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
@@ -130,7 +156,7 @@ struct TbStream {
         (void)dummy;
         const int sa = modn<2>(U - s), sb = modn<2>(U - s - 1);
         const int64_t row = i - s - 1;  // row of level s+1 computed now
-        const bool ok = !EDGE || in_interior(gx0 + row, nx);
+        const bool ok = !ROWCHK || row_in(row, rlo, rhi);
         const float4 cn = upd(R[s][sa], R[s][sb], c, ok);
         if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane, want_resid);
         R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
@@ -147,14 +173,14 @@ struct TbStream {
 #pragma unroll
       for (int s = 1; s < K; ++s) {
         const int rs = STEP * s;  // this level's row is i - rs
-        const bool ok = !EDGE || in_interior(gx0 + (i - rs), nx);
+        const bool ok = !ROWCHK || row_in(i - rs, rlo, rhi);
         R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
                                        R[s - 1][modn<RING>(U - rs)],
                                        R[s - 1][modn<RING>(U - rs + 1)], ok);
       }
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
-      const bool ok = !EDGE || in_interior(gx0 + ro, nx);
+      const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
       const float4& b = R[K - 1][modn<RING>(U - rK)];
       const float4 out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
@@ -163,35 +189,35 @@ struct TbStream {
   }
 
   template <int T, int S>
-  __device__ __forceinline__ void ramp_levels(int64_t i, int64_t gx0, int64_t nx,
-                                              const RowUpdate<EDGE>& upd) {
+  __device__ __forceinline__ void ramp_levels(int64_t i, int rlo, int rhi,
+                                              const RowUpdate<MODE>& upd) {
     if constexpr (S < K) {
       if constexpr (2 * S <= T) {
-        const bool ok = !EDGE || in_interior(gx0 + (i - S), nx);
+        const bool ok = !ROWCHK || row_in(i - S, rlo, rhi);
         R[S][modn<3>(T - S)] = upd(R[S - 1][modn<3>(T - S - 1)], R[S - 1][modn<3>(T - S)],
                                    R[S - 1][modn<3>(T - S + 1)], ok);
       }
-      ramp_levels<T, S + 1>(i, gx0, nx, upd);
+      ramp_levels<T, S + 1>(i, rlo, rhi, upd);
     }
   }
   template <int T>
   __device__ __forceinline__ void ramp(int64_t first_in, const float* __restrict__ src,
-                                       int64_t pitch, int64_t last_in, int64_t gx0, int64_t nx,
-                                       const RowUpdate<EDGE>& upd) {
+                                       int64_t pitch, int64_t last_in, int rlo, int rhi,
+                                       const RowUpdate<MODE>& upd) {
     if constexpr (T < 2 * K) {
       constexpr int U = T % 3;
       const int64_t i = first_in + T;
       R[0][U] = P[U];
       P[U] = *reinterpret_cast<const float4*>(src + min(i + 3, last_in) * pitch);
-      ramp_levels<T, 1>(i, gx0, nx, upd);
+      ramp_levels<T, 1>(i, rlo, rhi, upd);
       __builtin_amdgcn_sched_barrier(0);
-      ramp<T + 1>(first_in, src, pitch, last_in, gx0, nx, upd);
+      ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
     }
   }
 
   __device__ __forceinline__ void run(const float* __restrict__ src, float* __restrict__ dst,
-                                      int64_t pitch, int64_t rb, int64_t re, int64_t gx0,
-                                      int64_t nx, bool store_lane, const RowUpdate<EDGE>& upd,
+                                      int64_t pitch, int64_t rb, int64_t re, int rlo, int rhi,
+                                      bool store_lane, const RowUpdate<MODE>& upd,
                                       bool want_resid) {
     // src/dst are offset to this lane's column; rows are local rows.
     const int64_t first_in = rb - K, last_in = re + K - 1;
@@ -210,34 +236,42 @@ struct TbStream {
       // 2s useless rows per level per chunk (a third of all work for short
       // chunks).  The ramp is unrolled at compile time, one scheduling
       // region per iteration (keeps register pressure at the loop's level).
-      ramp<0>(first_in, src, pitch, last_in, gx0, nx, upd);
+      ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
       constexpr int U0 = (2 * K) % 3;
       for (int64_t t = 2 * K; t < T; t += 3) {
         const int64_t i = first_in + t;
-        body<U0>(i, t, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-        body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane,
+        body<U0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
+        body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
                            upd, want_resid);
-        body<(U0 + 2) % 3>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane,
+        body<(U0 + 2) % 3>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
                            upd, want_resid);
       }
       return;
     }
     for (int64_t t = 0; t < T; t += RING) {
       const int64_t i = first_in + t;
-      body<0>(i, t, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
-      body<1>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd, want_resid);
+      body<0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
+      body<1>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
       if constexpr (RING >= 3)
-        body<2>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd,
+        body<2>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
                 want_resid);
       if constexpr (RING == 4)
-        body<3>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, gx0, nx, store_lane, upd,
+        body<3>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
                 want_resid);
     }
   }
 };
 
+// Register budget: waves per SIMD each instantiation must keep (the edge
+// path and the ramp otherwise inflate the allocation for every wave).
 template <int K, int LAG>
-__global__ __launch_bounds__(256) void tb_kernel(TbArgs a) {
+constexpr int tb_waves_per_simd() {
+  if (LAG == 2) return K <= 4 ? 4 : 2;
+  return K <= 2 ? 6 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 8 ? 3 : 2;
+}
+
+template <int K, int LAG>
+__global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
   constexpr int KK = (K + 3) & ~3;
   constexpr int W = 256 - 2 * KK;
   const int lane = threadIdx.x & 63;
@@ -266,24 +300,45 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs a) {
   // global interior cell, so no Dirichlet masking is needed.
   const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
   const int64_t gx_lo = g.gx0 + rb - K, gx_hi = g.gx0 + re + K - 1;
-  const bool interior = gy_lo >= 1 && gy_hi <= g.ny - 2 && gx_lo >= 1 && gx_hi <= g.nx - 2;
-  unsigned m;
-  if (interior) {
-    RowUpdate<false> upd{g.cx, g.cy, true, true, true, true};
-    TbStream<K, LAG, false> st;
-    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
+  // Updatable local rows (global 1..nx-2), clamped into int32.
+  const int rlo = int(max<int64_t>(1 - g.gx0, -(int64_t(1) << 30)));
+  const int rhi = int(min<int64_t>(g.nx - 2 - g.gx0, int64_t(1) << 30));
+  unsigned m = 0;
+  // Which Dirichlet mode this wave needs (all wave-uniform).
+  const bool rows_in = gx_lo >= 1 && gx_hi <= g.nx - 2;
+  const bool left = gy_lo < 1, right = gy_hi > g.ny - 2;
+  int mode = kModeGeneric;
+  if (rows_in && !left && !right) mode = 0;
+  else if (rows_in && left && !right && g.gy0 == 0) mode = 1;
+  else if (rows_in && right && !left) mode = 2 + int((g.ny - 1 - g.gy0) & 3);
+  const int64_t gy = g.gy0 + col;
+  auto go = [&](auto mode_c) {
+    constexpr int MD = decltype(mode_c)::value;
+    RowUpdate<MD> upd;
+    upd.cx = g.cx;
+    upd.cy = g.cy;
+    if constexpr (MD == kModeGeneric) {
+      upd.cm0 = in_interior(gy, g.ny);
+      upd.cm1 = in_interior(gy + 1, g.ny);
+      upd.cm2 = in_interior(gy + 2, g.ny);
+      upd.cm3 = in_interior(gy + 3, g.ny);
+    } else if constexpr (MD == 1) {
+      upd.cm0 = gy == 0;  // element 0 of this lane is global column 0
+    } else if constexpr (MD >= 2) {
+      upd.cm0 = gy <= g.ny - 1 && g.ny - 1 < gy + 4;  // this lane holds column ny-1
+    }
+    TbStream<K, LAG, MD> st;
+    st.run(src, dst, g.pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
     m = st.m;
-  } else {
-    const int64_t gy = g.gy0 + col;
-    RowUpdate<true> upd{g.cx,
-                        g.cy,
-                        in_interior(gy, g.ny),
-                        in_interior(gy + 1, g.ny),
-                        in_interior(gy + 2, g.ny),
-                        in_interior(gy + 3, g.ny)};
-    TbStream<K, LAG, true> st;
-    st.run(src, dst, g.pitch, rb, re, g.gx0, g.nx, store_lane, upd, want_resid);
-    m = st.m;
+  };
+  switch (mode) {
+    case 0: go(std::integral_constant<int, 0>{}); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    default: go(std::integral_constant<int, kModeGeneric>{}); break;
   }
   if (want_resid) wave_max_atomic(m, a.resid);
 }

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$PWD
-ARGS=${ARGS:-"--depth 8 --variant 2 --waves 0 --launches 6"}
+ARGS=${ARGS:-"--depth 8 --variant 7 --waves 0 --launches 6"}
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 cd /tmp

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=200, help="steps per timed sample")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--interior", action="store_true",
+                    help="place the block inside a larger plate: no wave touches the boundary")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = args.n
@@ -36,7 +38,7 @@ def main():
     variants = [int(x) for x in args.variants.split(",")]
     waves = [int(x) for x in args.waves.split(",")]
     H = max(depths)
-    g = ops.Geom(nx=nx, ny=n)
+    g = ops.Geom(nx=nx, ny=n) if not args.interior else ops.Geom(nx=4 * nx, ny=4 * n, gx0=nx, gy0=n)
     a = ops.Field(nx, n, H, dev)
     b = ops.Field(nx, n, H, dev)
     ops.init_field(a, g, "random", 1)
