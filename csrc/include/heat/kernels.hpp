@@ -31,7 +31,7 @@ struct StencilGeom {
 };
 
 // Depths the temporally blocked kernel is instantiated for.
-constexpr int kTbMaxDepth = 16;
+constexpr int kTbMaxDepth = 8;  // deeper lost every sweep (register bound)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.
 int tb_strip_width(int k);

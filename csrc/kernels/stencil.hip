@@ -111,7 +111,7 @@ int grid_1d(int64_t n) { return int(std::min<int64_t>(ceil_div(n, 256), 256 * 16
 }  // namespace
 
 bool tb_depth_supported(int k) {
-  return (k >= 1 && k <= 8) || k == 10 || k == 12 || k == 16;
+  return k >= 1 && k <= kTbMaxDepth;
 }
 
 int tb_strip_width(int k) { return 256 - 2 * int(round_up(k, 4)); }
@@ -180,7 +180,7 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
-  HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);
+  HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   if (variant < 0) variant = tb_default_variant();
   const int lag = tb_variant_lag(variant);
   if (waves_target <= 0) {
@@ -205,21 +205,62 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   const char* ml = std::getenv("HEAT_TB_MINLEN");
   const int64_t min_len = ml && *ml ? std::max(1, std::atoi(ml)) : std::max<int64_t>(depth, 8);
   int64_t len = std::max<int64_t>(min_len, ceil_div(total_strip_rows, waves_target));
+  // Rows whose chunk window reaches the global top/bottom row run the
+  // generic (masked) path, which is slower: give them shorter chunks, as
+  // separate sub-boxes, so those waves do not set the tail of the launch.
+  static const double edge_frac = [] {
+    const char* e = std::getenv("HEAT_TB_EDGE_FRAC");
+    return e && *e ? std::atof(e) : 0.75;
+  }();
   int n = 0, waves = 0;
-  for (int b = 0; b < nbox; ++b) {
-    const Box& B = boxes[b];
-    if (B.empty()) continue;
-    HEAT_CHECK(B.c0 % 4 == 0, "TB box column start %lld not a multiple of 4", (long long)B.c0);
-    TbBox& t = args.box[n++];
-    t.r0 = B.r0;
-    t.r1 = B.r1;
-    t.c0 = B.c0;
-    t.c1 = B.c1;
-    t.nstrips = int(ceil_div(B.cols(), W));
-    t.chunk_len = int(std::min<int64_t>(len, B.rows()));
-    t.nchunks = int(ceil_div(B.rows(), t.chunk_len));
-    t.wave_begin = waves;
-    waves += t.nstrips * t.nchunks;
+  auto plan = [&](int64_t L) {
+    const int64_t edge_len = std::max<int64_t>(std::min<int64_t>(min_len, L),
+                                               int64_t(double(L) * edge_frac));
+    n = 0;
+    waves = 0;
+    auto add = [&](const Box& B, int64_t clen) {
+      if (B.empty()) return;
+      HEAT_CHECK(n < tbdetail::kMaxBoxes, "too many TB sub-boxes");
+      TbBox& t = args.box[n++];
+      t.r0 = B.r0;
+      t.r1 = B.r1;
+      t.c0 = B.c0;
+      t.c1 = B.c1;
+      t.nstrips = int(ceil_div(B.cols(), W));
+      t.chunk_len = int(std::min<int64_t>(clen, B.rows()));
+      t.nchunks = int(ceil_div(B.rows(), t.chunk_len));
+      t.wave_begin = waves;
+      waves += t.nstrips * t.nchunks;
+    };
+    for (int b = 0; b < nbox; ++b) {
+      const Box& B = boxes[b];
+      if (B.empty()) continue;
+      HEAT_CHECK(B.c0 % 4 == 0, "TB box column start %lld not a multiple of 4", (long long)B.c0);
+      Box mid = B;
+      if (edge_len < L && B.rows() > 2 * L) {
+        // Local rows whose window [r - depth, r + depth] touches global row 0 / nx-1.
+        const int64_t top_end = 1 - g.gx0 + depth;          // first row clear of the top
+        const int64_t bot_begin = g.nx - 2 - g.gx0 - depth;  // last row clear of the bottom
+        if (B.r0 < top_end) {
+          const int64_t e = std::min(B.r1, std::max(top_end, B.r0 + edge_len));
+          add(Box{B.r0, e, B.c0, B.c1}, edge_len);
+          mid.r0 = e;
+        }
+        if (B.r1 - 1 > bot_begin && mid.r1 > mid.r0) {
+          const int64_t s0 = std::max(mid.r0, std::min(bot_begin + 1, B.r1 - edge_len));
+          add(Box{s0, B.r1, B.c0, B.c1}, edge_len);
+          mid.r1 = s0;
+        }
+      }
+      add(mid, L);
+    }
+  };
+  // Keep the total within waves_target (whole resident rounds): a few extra
+  // waves would form a nearly empty extra round.
+  plan(len);
+  for (int it = 0; it < 8 && waves > waves_target; ++it) {
+    len = std::max(len + 1, ceil_div(len * int64_t(waves), int64_t(waves_target)));
+    plan(len);
   }
   if (n == 0) return;
   args.nbox = n;

@@ -15,13 +15,15 @@ struct TbBox {
   int nstrips, nchunks, chunk_len, wave_begin;
 };
 
+constexpr int kMaxBoxes = 16;
+
 struct TbArgs {
   const float* src;
   float* dst;
   unsigned* resid;
   StencilGeom g;
   int nbox, total_waves;
-  TbBox box[5];
+  TbBox box[kMaxBoxes];
 };
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   if (wave >= a.total_waves) return;
   int bi = 0;
 #pragma unroll
-  for (int j = 1; j < 5; ++j)
+  for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
     if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
   const TbBox bx = a.box[bi];
   const int w = wave - bx.wave_begin;
@@ -378,39 +378,7 @@ int occupancy(int depth, int lag) {
     case 6: return occ_k<6, 3>();
     case 7: return occ_k<7, 3>();
     case 8: return occ_k<8, 3>();
-    case 10: return occ_k<10, 3>();
-    case 12: return occ_k<12, 3>();
-    case 16: return occ_k<16, 3>();
     default: return 1;
-    }
-  }
-  if (lag == 0) {
-    switch (depth) {
-      case 1: return occ_k<1, 0>();
-      case 2: return occ_k<2, 0>();
-      case 3: return occ_k<3, 0>();
-      case 4: return occ_k<4, 0>();
-      case 5: return occ_k<5, 0>();
-      case 6: return occ_k<6, 0>();
-      case 7: return occ_k<7, 0>();
-      case 8: return occ_k<8, 0>();
-      case 10: return occ_k<10, 0>();
-      case 12: return occ_k<12, 0>();
-      case 16: return occ_k<16, 0>();
-      default: return 1;
-    }
-  }
-  if (lag == 2) {
-    switch (depth) {
-      case 1: return occ_k<1, 2>();
-      case 2: return occ_k<2, 2>();
-      case 3: return occ_k<3, 2>();
-      case 4: return occ_k<4, 2>();
-      case 5: return occ_k<5, 2>();
-      case 6: return occ_k<6, 2>();
-      case 7: return occ_k<7, 2>();
-      case 8: return occ_k<8, 2>();
-      default: break;
     }
   }
   switch (depth) {
@@ -422,14 +390,14 @@ int occupancy(int depth, int lag) {
     case 6: return occ_k<6, 1>();
     case 7: return occ_k<7, 1>();
     case 8: return occ_k<8, 1>();
-    case 10: return occ_k<10, 1>();
-    case 12: return occ_k<12, 1>();
-    case 16: return occ_k<16, 1>();
     default: return 1;
   }
 }
 
-// Returns false if (depth, lag) is not instantiated.
+// Returns false if (depth, lag) is not instantiated.  Only the skew-1
+// pipelines (LAG 1, and LAG 3 = LAG 1 + ramp) are instantiated: the skew-2
+// (LAG 2) and 2-slot (LAG 0) forms lost every sweep (profiles/tb_sweep_*.json)
+// and only cost build time.
 bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
   if (lag == 3) {
   switch (depth) {
@@ -441,39 +409,7 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
     case 6: launch_k<6, 3>(args, st); return true;
     case 7: launch_k<7, 3>(args, st); return true;
     case 8: launch_k<8, 3>(args, st); return true;
-    case 10: launch_k<10, 3>(args, st); return true;
-    case 12: launch_k<12, 3>(args, st); return true;
-    case 16: launch_k<16, 3>(args, st); return true;
     default: return false;
-    }
-  }
-  if (lag == 0) {
-    switch (depth) {
-      case 1: launch_k<1, 0>(args, st); return true;
-      case 2: launch_k<2, 0>(args, st); return true;
-      case 3: launch_k<3, 0>(args, st); return true;
-      case 4: launch_k<4, 0>(args, st); return true;
-      case 5: launch_k<5, 0>(args, st); return true;
-      case 6: launch_k<6, 0>(args, st); return true;
-      case 7: launch_k<7, 0>(args, st); return true;
-      case 8: launch_k<8, 0>(args, st); return true;
-      case 10: launch_k<10, 0>(args, st); return true;
-      case 12: launch_k<12, 0>(args, st); return true;
-      case 16: launch_k<16, 0>(args, st); return true;
-      default: return false;
-    }
-  }
-  if (lag == 2) {
-    switch (depth) {
-      case 1: launch_k<1, 2>(args, st); return true;
-      case 2: launch_k<2, 2>(args, st); return true;
-      case 3: launch_k<3, 2>(args, st); return true;
-      case 4: launch_k<4, 2>(args, st); return true;
-      case 5: launch_k<5, 2>(args, st); return true;
-      case 6: launch_k<6, 2>(args, st); return true;
-      case 7: launch_k<7, 2>(args, st); return true;
-      case 8: launch_k<8, 2>(args, st); return true;
-      default: break;  // deeper: LAG 1 (register budget)
     }
   }
   switch (depth) {
@@ -485,9 +421,6 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
     case 6: launch_k<6, 1>(args, st); return true;
     case 7: launch_k<7, 1>(args, st); return true;
     case 8: launch_k<8, 1>(args, st); return true;
-    case 10: launch_k<10, 1>(args, st); return true;
-    case 12: launch_k<12, 1>(args, st); return true;
-    case 16: launch_k<16, 1>(args, st); return true;
     default: return false;
   }
 }

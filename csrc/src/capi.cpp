@@ -124,7 +124,7 @@ extern "C" {
 const char* heat_last_error(void) { return g_err.c_str(); }
 int heat_abi_version(void) { return HEAT_ABI_VERSION; }
 const char* heat_build_info(void) {
-  return "libheat: gfx950 HIP kernels (naive, tb depths 1-8,10,12,16), RCCL/TCP/callback transports";
+  return "libheat: gfx950 HIP kernels (naive, tb depths 1-8), RCCL/TCP/callback transports";
 }
 
 int heat_rccl_unique_id(uint8_t out[128]) {

@@ -49,8 +49,8 @@ def test_naive_step_vs_torch(gpu):
     torch.testing.assert_close(b.owned(), ref, rtol=1e-6, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
-@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16])
+@pytest.mark.parametrize("variant", [0, 3, 4, 7])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     lx, ly = 203, 517  # odd sizes: partial strips and chunks
     g, a, b = _fields(lx, ly, depth, gpu)

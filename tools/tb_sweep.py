@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200, help="steps per timed sample")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--plate-nx", type=int, default=0,
+                    help="treat the block as rows [gx0, gx0+nx) of a plate with this many rows")
+    ap.add_argument("--gx0", type=int, default=0)
     ap.add_argument("--interior", action="store_true",
                     help="place the block inside a larger plate: no wave touches the boundary")
     args = ap.parse_args()
@@ -39,6 +42,8 @@ def main():
     waves = [int(x) for x in args.waves.split(",")]
     H = max(depths)
     g = ops.Geom(nx=nx, ny=n) if not args.interior else ops.Geom(nx=4 * nx, ny=4 * n, gx0=nx, gy0=n)
+    if args.plate_nx:
+        g = ops.Geom(nx=args.plate_nx, ny=n, gx0=args.gx0)
     a = ops.Field(nx, n, H, dev)
     b = ops.Field(nx, n, H, dev)
     ops.init_field(a, g, "random", 1)
