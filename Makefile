@@ -14,7 +14,7 @@ CXXSTD  := -std=c++17
 COMMON  := $(CXXSTD) -O3 -fPIC -Wall -Wno-unused-result -Icsrc/include -mfma -mavx2 \
            -fopenmp -D__HIP_PLATFORM_AMD__
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LDFLAGS := -fopenmp -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+LDFLAGS := -fopenmp -L$(ROCM)/lib -lrccl -ldl -Wl,-rpath,$(ROCM)/lib
 
 SRCS_CPP := $(wildcard csrc/src/*.cpp)
 SRCS_HIP := $(wildcard csrc/kernels/*.hip)
@@ -55,3 +55,42 @@ clean:
 	rm -rf $(BUILD) $(LIBDIR)/libheat.so
 
 .PHONY: all asm resources clean
+
+# Host-only self-test of the CPU components, plain and under ASan/UBSan.
+SELFTEST_SRCS := csrc/tests/selftest.cpp csrc/src/common.cpp csrc/src/topology.cpp \
+                 csrc/src/io.cpp csrc/src/cpu_backend.cpp
+$(BUILD)/selftest: $(SELFTEST_SRCS) $(HDRS)
+	@mkdir -p $(BUILD)
+	g++ -std=c++17 -O2 -g -Wall -Icsrc/include -mfma -mavx2 -fopenmp $(SELFTEST_SRCS) -o $@
+$(BUILD)/selftest-asan: $(SELFTEST_SRCS) $(HDRS)
+	@mkdir -p $(BUILD)
+	g++ -std=c++17 -O1 -g -Wall -Icsrc/include -mfma -mavx2 -fopenmp \
+	  -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all \
+	  $(SELFTEST_SRCS) -o $@
+selftest: $(BUILD)/selftest
+	$(BUILD)/selftest
+selftest-asan: $(BUILD)/selftest-asan
+	ASAN_OPTIONS=detect_leaks=1 $(BUILD)/selftest-asan
+.PHONY: selftest selftest-asan
+
+# Reference-compatible program names (mpi/Makefile:12-22, cuda/Makefile:13):
+#   make ref-variants SIZE=900 STEPS=10000 STEP=20 THREADS=4
+# writes build/ref/{heat_N,heat_omp_N,heat_con_N,heat_con_omp_N,cuda_heat}; run
+# them as `NP=4 build/ref/heat_omp_900` (NP processes, like mpirun -np).
+SIZE ?= 900
+STEPS ?= 10000
+STEP ?= 20
+THREADS ?= 4
+ref-variants: $(BUILD)/heat
+	@mkdir -p $(BUILD)/ref
+	@for v in "heat_$(SIZE):--threads 1" "heat_omp_$(SIZE):--threads $(THREADS)" \
+	          "heat_con_$(SIZE):--threads 1 --converge --check-interval $(STEP)" \
+	          "heat_con_omp_$(SIZE):--threads $(THREADS) --converge --check-interval $(STEP)"; do \
+	  name=$${v%%:*}; args=$${v#*:}; \
+	  printf '#!/bin/bash\n# %s: reference mpi/Makefile variant\nexec python3 -m torch.distributed.run --no-python --standalone --nproc-per-node $${NP:-1} %s --backend cpu --nx %s --ny %s --steps %s --naming mpi %s "$$@"\n' \
+	    "$$name" "$(abspath $(BUILD)/heat)" $(SIZE) $(SIZE) $(STEPS) "$$args" > $(BUILD)/ref/$$name; \
+	  chmod +x $(BUILD)/ref/$$name; done
+	@printf '#!/bin/bash\n# cuda_heat: reference cuda/Makefile program\nexec %s --backend hip --nx %s --ny %s --steps %s --naming cuda "$$@"\n' \
+	  "$(abspath $(BUILD)/heat)" $(SIZE) $(SIZE) $(STEPS) > $(BUILD)/ref/cuda_heat; chmod +x $(BUILD)/ref/cuda_heat
+	@ls $(BUILD)/ref
+.PHONY: ref-variants

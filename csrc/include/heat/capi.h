@@ -96,6 +96,8 @@ int heat_solver_load_owned(heat_solver* s, const float* host, int64_t host_pitch
 /* rank 0: host must hold nx*ny floats; other ranks: host may be NULL */
 int heat_solver_gather(heat_solver* s, float* host);
 int heat_solver_checksum(heat_solver* s, heat_checksum* out);
+/* rank 0: full holds nx*ny floats (row-major); other ranks: full may be NULL */
+int heat_solver_scatter(heat_solver* s, const float* full, int64_t step);
 int heat_solver_write_bin(heat_solver* s, const char* path);
 int heat_solver_read_bin(heat_solver* s, const char* path);
 int heat_solver_barrier(heat_solver* s);

@@ -71,6 +71,19 @@ int tb_resident_waves(int depth, int variant);
 void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hipStream_t st);
 void unpack_box(const float* buf, float* origin, int64_t pitch, const Box& box, hipStream_t st);
 
+// Order-independent checksum of the owned block, accumulated on the device
+// into out (zeroed by the caller): hash (u64, wrapping sum of
+// mix64(global index, bits)), sum (f64), min/max (order-preserving int keys).
+struct DeviceChecksum {
+  unsigned long long hash;
+  double sum;
+  int min_key, max_key;
+  unsigned long long count;
+};
+void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, int64_t ox,
+                    int64_t oy, int64_t ny, DeviceChecksum* out, hipStream_t st);
+float checksum_key_to_float(int key);
+
 // Max |a-b| over a box (standalone residual), atomically into *resid.
 void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,
                   hipStream_t st);

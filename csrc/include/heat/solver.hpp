@@ -78,6 +78,10 @@ class Solver {
   void load_owned(const float* host, int64_t host_pitch, int64_t step);
   // Full grid on rank 0 (nx*ny row-major); empty vector on other ranks.
   std::vector<float> gather_root();
+  // Inverse of gather_root: rank 0 holds the full nx*ny grid (`full`, ignored
+  // elsewhere) and every rank receives its block (the reference's master
+  // scatter, mpi/...c:100-127).  Collective.
+  void scatter_root(const float* full, int64_t step);
   // Global order-independent checksum (identical on every rank).
   Checksum checksum();
   // Binary output / checkpoint of the current state (all ranks call).
@@ -134,6 +138,7 @@ class Solver {
   unsigned* d_resid_ = nullptr;
   float* h_resid_ = nullptr;
   void* d_scratch_ = nullptr;
+  void* d_checksum_ = nullptr;
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
     int cur_after = 0;

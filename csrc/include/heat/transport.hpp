@@ -57,6 +57,8 @@ class Transport {
   virtual void allreduce_sum_f64(double* buf, int count, hipStream_t st) = 0;
   virtual void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) = 0;
   virtual void barrier() = 0;
+  // Throws if the transport has failed asynchronously (e.g. a dead peer).
+  virtual void check() {}
   virtual const char* name() const = 0;
 };
 

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -104,6 +105,50 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
     for (int64_t r = box.r0 + blockIdx.y * 4 + threadIdx.y; r < box.r1; r += gridDim.y * 4)
       m = max(m, __float_as_uint(fabsf(a[r * pitch + c] - b[r * pitch + c])));
   wave_max_atomic(m, resid);
+}
+
+__device__ __forceinline__ int float_key(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : (i ^ 0x7FFFFFFF);
+}
+
+__global__ __launch_bounds__(256) void checksum_kernel(const float* __restrict__ origin,
+                                                       int64_t pitch, int64_t lx, int64_t ly,
+                                                       int64_t ox, int64_t oy, int64_t ny,
+                                                       DeviceChecksum* out) {
+  unsigned long long h = 0, cnt = 0;
+  double sum = 0.0;
+  int mn = 0x7FFFFFFF, mx = int(0x80000000);
+  for (int64_t r = blockIdx.y; r < lx; r += gridDim.y) {
+    const float* row = origin + r * pitch;
+    const uint64_t gbase = uint64_t(ox + r) * uint64_t(ny) + uint64_t(oy);
+    for (int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; c < ly;
+         c += int64_t(gridDim.x) * blockDim.x) {
+      const float v = row[c];
+      const uint32_t bits = __float_as_uint(v);
+      h += mix64((gbase + uint64_t(c)) * 0x100000001B3ull ^ bits);
+      sum += double(v);
+      const int k = float_key(v);
+      mn = min(mn, k);
+      mx = max(mx, k);
+      ++cnt;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    h += __shfl_xor(h, off);
+    cnt += __shfl_xor(cnt, off);
+    sum += __shfl_xor(sum, off);
+    mn = min(mn, __shfl_xor(mn, off));
+    mx = max(mx, __shfl_xor(mx, off));
+  }
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(&out->hash, h);
+    atomicAdd(&out->count, cnt);
+    atomicAdd(&out->sum, sum);
+    atomicMin(&out->min_key, mn);
+    atomicMax(&out->max_key, mx);
+  }
 }
 
 int grid_1d(int64_t n) { return int(std::min<int64_t>(ceil_div(n, 256), 256 * 16)); }
@@ -281,6 +326,23 @@ void unpack_box(const float* buf, float* origin, int64_t pitch, const Box& box, 
   if (box.empty()) return;
   hipLaunchKernelGGL(unpack_kernel, dim3(grid_1d(box.rows() * box.cols())), dim3(256), 0, st,
                      buf, origin, pitch, box);
+  HIP_CHECK(hipGetLastError());
+}
+
+float checksum_key_to_float(int key) {
+  const int i = key >= 0 ? key : (key ^ 0x7FFFFFFF);
+  float f;
+  std::memcpy(&f, &i, 4);
+  return f;
+}
+
+void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, int64_t ox,
+                    int64_t oy, int64_t ny, DeviceChecksum* out, hipStream_t st) {
+  if (lx <= 0 || ly <= 0) return;
+  dim3 grid(unsigned(std::min<int64_t>(ceil_div(ly, 256), 64)),
+            unsigned(std::min<int64_t>(lx, 4096)));
+  hipLaunchKernelGGL(checksum_kernel, grid, dim3(256), 0, st, origin, pitch, lx, ly, ox, oy, ny,
+                     out);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -16,20 +16,6 @@
 
 namespace heat {
 
-void throw_error(const char* file, int line, const std::string& msg) {
-  const char* base = std::strrchr(file, '/');
-  throw Error(strprintf("%s:%d: %s", base ? base + 1 : file, line, msg.c_str()));
-}
-
-std::string strprintf(const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  std::vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  return buf;
-}
-
 const char* init_mode_name(InitMode m) {
   switch (m) {
     case InitMode::RefWrap: return "ref-wrap";
@@ -258,6 +244,10 @@ int heat_solver_checksum(heat_solver* s, heat_checksum* out) {
     out->max = c.max;
     out->count = c.count;
   });
+}
+
+int heat_solver_scatter(heat_solver* s, const float* full, int64_t step) {
+  return guard([&] { s->s->scatter_root(full, step); });
 }
 
 int heat_solver_write_bin(heat_solver* s, const char* path) {

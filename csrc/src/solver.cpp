@@ -10,6 +10,7 @@
 #include "heat/common.hpp"
 #include "heat/cpu_backend.hpp"
 #include "heat/kernels.hpp"
+#include "heat/trace.hpp"
 
 namespace heat {
 namespace {
@@ -89,6 +90,7 @@ void Solver::alloc() {
     HIP_CHECK(hipMalloc(&d_resid_, 256));
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
+    HIP_CHECK(hipMalloc(&d_checksum_, 256));
     if (staged_) {
       stage_bytes_ = std::max<size_t>(size_t(H_) * size_t(L_.pitch), ew_elems) * 4;
       for (int i = 0; i < 4; ++i) {
@@ -128,6 +130,7 @@ void Solver::free_all() {
     if (d_resid_) (void)hipFree(d_resid_);
     if (h_resid_) (void)hipHostFree(h_resid_);
     if (d_scratch_) (void)hipFree(d_scratch_);
+    if (d_checksum_) (void)hipFree(d_checksum_);
     for (auto e : {ev_ready_, ev_halo_, ev_t0_, ev_t1_})
       if (e) (void)hipEventDestroy(e);
     if (s_comp_) (void)hipStreamDestroy(s_comp_);
@@ -176,6 +179,7 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
 // halo exchange
 // ---------------------------------------------------------------------------
 void Solver::exchange(int buf, int k, hipStream_t st) {
+  TraceRange trace("heat.exchange");
   float* f = field_[buf];
   const auto& nb = blk_.nbr;
   const int64_t lx = blk_.lx, ly = blk_.ly, pitch = L_.pitch;
@@ -361,9 +365,11 @@ void Solver::enqueue_segment(int64_t n, bool resid) {
 }
 
 float Solver::finish_resid() {
+  TraceRange trace("heat.residual_wait");
   float r;
   if (on_gpu()) {
     HIP_CHECK(hipStreamSynchronize(s_comp_));
+    tr_->check();
     std::memcpy(&r, h_resid_, 4);
     if (!tr_->device_memory()) tr_->allreduce_max(&r, 1, nullptr);
   } else {
@@ -384,6 +390,7 @@ bool Solver::converged_value(float r) const {
 }
 
 RunStats Solver::run(int64_t steps) {
+  TraceRange trace("heat.run");
   RunStats s;
   HEAT_CHECK(steps >= 0, "negative step count");
   const int64_t p0 = stat_passes_, e0 = stat_exchanges_;
@@ -424,6 +431,7 @@ RunStats Solver::run(int64_t steps) {
       const int64_t step_before = step_;
       if (it == graphs_.end()) {
         const int64_t p_before = stat_passes_, e_before = stat_exchanges_;
+        TraceRange trace_capture("heat.capture");
         hipGraph_t graph;
         HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
         capturing_ = true;
@@ -473,6 +481,7 @@ RunStats Solver::run(int64_t steps) {
     }
   }
   synchronize();
+  tr_->check();
   s.seconds = now_s() - t0;
   s.total_steps = step_;
   s.passes = stat_passes_ - p0;
@@ -518,7 +527,58 @@ void Solver::load_owned(const float* host, int64_t host_pitch, int64_t step) {
   step_ = step;
 }
 
+void Solver::scatter_root(const float* full, int64_t step) {
+  TraceRange tr("heat.scatter");
+  const int rank = tr_->rank(), world = tr_->world();
+  const bool dev = tr_->device_memory();
+  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+  int64_t max_block = 0;
+  for (int r = 0; r < world; ++r) {
+    Block b = make_block(cart_, r, P_.nx, P_.ny);
+    max_block = std::max(max_block, b.lx * b.ly);
+  }
+  float* dbuf = nullptr;
+  if (dev && world > 1) HIP_CHECK(hipMalloc(&dbuf, size_t(max_block) * 4));
+  auto cut = [&](const Block& b, float* dst) {
+    for (int64_t r = 0; r < b.lx; ++r)
+      std::memcpy(dst + r * b.ly, full + (b.ox + r) * P_.ny + b.oy, size_t(b.ly) * 4);
+  };
+  if (rank == 0) {
+    HEAT_CHECK(full != nullptr, "scatter_root: rank 0 needs the full grid");
+    cut(blk_, mine.data());
+    std::vector<float> tmp(static_cast<size_t>(max_block));
+    for (int r = 1; r < world; ++r) {
+      Block b = make_block(cart_, r, P_.nx, P_.ny);
+      cut(b, tmp.data());
+      const size_t bytes = size_t(b.lx * b.ly) * 4;
+      if (dev) {
+        HIP_CHECK(hipMemcpyAsync(dbuf, tmp.data(), bytes, hipMemcpyHostToDevice, s_comp_));
+        Msg m{r, dbuf, bytes, nullptr, 0};
+        tr_->sendrecv(&m, 1, s_comp_);
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+      } else {
+        Msg m{r, tmp.data(), bytes, nullptr, 0};
+        tr_->sendrecv(&m, 1, nullptr);
+      }
+    }
+  } else {
+    const size_t bytes = mine.size() * 4;
+    if (dev) {
+      Msg m{0, nullptr, 0, dbuf, bytes};
+      tr_->sendrecv(&m, 1, s_comp_);
+      HIP_CHECK(hipMemcpyAsync(mine.data(), dbuf, bytes, hipMemcpyDeviceToHost, s_comp_));
+      HIP_CHECK(hipStreamSynchronize(s_comp_));
+    } else {
+      Msg m{0, nullptr, 0, mine.data(), bytes};
+      tr_->sendrecv(&m, 1, nullptr);
+    }
+  }
+  if (dbuf) HIP_CHECK(hipFree(dbuf));
+  load_owned(mine.data(), blk_.ly, step);
+}
+
 std::vector<float> Solver::gather_root() {
+  TraceRange trace("heat.gather");
   const int rank = tr_->rank(), world = tr_->world();
   std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
   copy_owned(mine.data(), blk_.ly);
@@ -591,9 +651,27 @@ void Solver::reduce_scalars(double* f64, int nf, uint64_t* u64, int nu, float* f
 }
 
 Checksum Solver::checksum() {
-  std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
-  copy_owned(mine.data(), blk_.ly);
-  Checksum c = checksum_block(mine.data(), blk_.ly, blk_.ox, blk_.oy, blk_.lx, blk_.ly, P_.ny);
+  TraceRange tr("heat.checksum");
+  Checksum c;
+  if (on_gpu()) {
+    // On the device: no host copy of the block (131072^2 grids are 68 GB).
+    auto* d = static_cast<gpu::DeviceChecksum*>(d_checksum_);
+    gpu::DeviceChecksum h{0, 0.0, 0x7FFFFFFF, int(0x80000000), 0};
+    HIP_CHECK(hipMemcpyAsync(d, &h, sizeof h, hipMemcpyHostToDevice, s_comp_));
+    gpu::checksum_block(field_[cur_], L_.pitch, blk_.lx, blk_.ly, blk_.ox, blk_.oy, P_.ny, d,
+                        s_comp_);
+    HIP_CHECK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    c.hash = h.hash;
+    c.sum = h.sum;
+    c.count = int64_t(h.count);
+    c.min = gpu::checksum_key_to_float(h.min_key);
+    c.max = gpu::checksum_key_to_float(h.max_key);
+  } else {
+    std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
+    copy_owned(mine.data(), blk_.ly);
+    c = checksum_block(mine.data(), blk_.ly, blk_.ox, blk_.oy, blk_.lx, blk_.ly, P_.ny);
+  }
   double f[1] = {c.sum};
   uint64_t u[2] = {c.hash, uint64_t(c.count)};
   float m[2] = {float(c.max), float(-c.min)};

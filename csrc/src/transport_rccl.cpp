@@ -74,6 +74,13 @@ class RcclTransport final : public Transport {
     HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipStreamDestroy(st));
   }
+  void check() override {
+    ncclResult_t async = ncclSuccess;
+    NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
+    if (async != ncclSuccess && async != ncclInProgress)
+      throw_error(__FILE__, __LINE__,
+                  std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+  }
   const char* name() const override { return "rccl"; }
 
  private:

@@ -56,6 +56,21 @@ void read_all(int fd, void* p, size_t n) {
   }
 }
 
+// IPv4 address of a host name or dotted quad ("localhost" from
+// torch.distributed.run --standalone included).
+in_addr resolve(const std::string& addr) {
+  in_addr a{};
+  if (inet_pton(AF_INET, addr.c_str(), &a) == 1) return a;
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  HEAT_CHECK(getaddrinfo(addr.c_str(), nullptr, &hints, &res) == 0 && res, "cannot resolve %s",
+             addr.c_str());
+  a = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+  freeaddrinfo(res);
+  return a;
+}
+
 int listen_on(const std::string& addr, int port, int* bound_port) {
   int fd = ::socket(AF_INET, SOCK_STREAM, 0);
   HEAT_CHECK(fd >= 0, "socket: %s", std::strerror(errno));
@@ -64,7 +79,7 @@ int listen_on(const std::string& addr, int port, int* bound_port) {
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
   sa.sin_port = htons(uint16_t(port));
-  HEAT_CHECK(inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) == 1, "bad address %s", addr.c_str());
+  sa.sin_addr = resolve(addr);
   HEAT_CHECK(::bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0, "bind %s:%d: %s",
              addr.c_str(), port, std::strerror(errno));
   HEAT_CHECK(::listen(fd, 128) == 0, "listen: %s", std::strerror(errno));
@@ -78,7 +93,7 @@ int connect_to(const std::string& addr, int port, double timeout_s) {
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
   sa.sin_port = htons(uint16_t(port));
-  HEAT_CHECK(inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) == 1, "bad address %s", addr.c_str());
+  sa.sin_addr = resolve(addr);
   auto t0 = std::chrono::steady_clock::now();
   while (true) {
     int fd = ::socket(AF_INET, SOCK_STREAM, 0);

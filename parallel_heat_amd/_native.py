@@ -112,6 +112,7 @@ _SIGS = {
     "heat_solver_load_owned": (c_int, [c_void_p, c_void_p, c_int64, c_int64]),
     "heat_solver_gather": (c_int, [c_void_p, c_void_p]),
     "heat_solver_checksum": (c_int, [c_void_p, POINTER(HeatChecksum)]),
+    "heat_solver_scatter": (c_int, [c_void_p, c_void_p, c_int64]),
     "heat_solver_write_bin": (c_int, [c_void_p, c_char_p]),
     "heat_solver_read_bin": (c_int, [c_void_p, c_char_p]),
     "heat_solver_barrier": (c_int, [c_void_p]),

@@ -188,6 +188,20 @@ class HeatSolver:
         _native.call("heat_solver_gather", self._h, None)
         return None
 
+    def scatter(self, grid: Optional[np.ndarray] = None, step: int = 0) -> None:
+        """Distribute a full (nx, ny) grid held by rank 0 to every rank's block
+        (the reference's master scatter, mpi/...c:100-127).  Collective; other
+        ranks pass None."""
+        if self.rank == 0:
+            if grid is None:
+                raise ValueError("rank 0 must pass the full grid")
+            g = np.ascontiguousarray(grid, dtype=np.float32)
+            if g.shape != (self.config.nx, self.config.ny):
+                raise ValueError(f"grid shape {g.shape} != {(self.config.nx, self.config.ny)}")
+            _native.call("heat_solver_scatter", self._h, g.ctypes.data, int(step))
+        else:
+            _native.call("heat_solver_scatter", self._h, None, int(step))
+
     def checksum(self) -> dict:
         c = _native.HeatChecksum()
         _native.call("heat_solver_checksum", self._h, ctypes.byref(c))

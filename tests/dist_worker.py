@@ -31,6 +31,9 @@ def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
     cfg = HeatConfig(**cfg_kwargs)
     s = HeatSolver(cfg, transport=transport, dist_info=DistInfo(rank, world, rank),
                    device=0 if cfg.backend == "hip" else None)
+    if cfg_kwargs.get("init") == "zero":  # start from a grid scattered by rank 0
+        from parallel_heat_amd.models import reference as R
+        s.scatter(R.init_grid(cfg.nx, cfg.ny, "random", 77) if rank == 0 else None)
     conv, conv_at, done = False, -1, 0
     for n in (chunks or [steps]):
         r = s.run(n)

@@ -124,3 +124,18 @@ def test_invalid_config():
         HeatConfig(nx=0).validate()
     with pytest.raises(ValueError):
         HeatConfig(init="bogus").validate()
+
+
+def test_scatter_single_rank():
+    cfg = HeatConfig(nx=21, ny=34, steps=0, init="zero", backend="cpu")
+    from parallel_heat_amd.models import reference as R
+    g0 = R.init_grid(21, 34, "random", 9)
+    with HeatSolver(cfg) as s:
+        s.scatter(g0, step=3)
+        assert s.step == 3
+        assert np.array_equal(s.gather(), g0)
+        s.run(10)
+        a = s.gather()
+    with HeatSolver(cfg.replace(init="random", seed=9)) as s:
+        s.run(10)
+        assert np.array_equal(s.gather(), a)

@@ -52,3 +52,10 @@ def test_mpi_compat_distributed(tmp_path):
     kw = {**BASE, "compat": "mpi", "steps": 10}
     res = run_world(2, kw, None, tmp_path)
     assert int(res["done"]) == 11
+
+
+def test_scatter_then_run_distributed(tmp_path):
+    kw = dict(nx=31, ny=27, steps=0, init="zero", backend="cpu", decomp="auto")
+    res = run_world(3, kw, 12, tmp_path)
+    ref, _ = single(dict(nx=31, ny=27, steps=0, init="random", seed=77, backend="cpu"), 12)
+    assert np.array_equal(res["grid"], ref)

@@ -77,3 +77,30 @@ def test_large_grid_smoke(gpu):
         cs = s.checksum()
     assert r.steps_done == 64 and np.isfinite(cs["sum"])
     assert torch.cuda.is_available()
+
+
+def test_device_checksum_matches_host(gpu):
+    cfg = HeatConfig(nx=300, ny=517, steps=20, init="random", backend="hip")
+    with HeatSolver(cfg) as s:
+        s.run()
+        cg = s.checksum()
+        g = s.gather()
+    with HeatSolver(cfg.replace(backend="cpu")) as c:
+        c.run()
+        cc = c.checksum()
+    assert cg["hash"] == cc["hash"] and cg["count"] == cc["count"]
+    assert cg["min"] == float(g.min()) and cg["max"] == float(g.max())
+    assert abs(cg["sum"] - cc["sum"]) <= 1e-9 * abs(cc["sum"]) + 1e-6
+
+
+def test_gpu_scatter(gpu):
+    from parallel_heat_amd.models import reference as R
+    g0 = R.init_grid(64, 300, "random", 5)
+    cfg = HeatConfig(nx=64, ny=300, steps=0, init="zero", backend="hip")
+    with HeatSolver(cfg) as s:
+        s.scatter(g0)
+        s.run(17)
+        a = s.gather()
+    with HeatSolver(cfg.replace(init="random", seed=5)) as s:
+        s.run(17)
+        assert np.array_equal(s.gather(), a)
