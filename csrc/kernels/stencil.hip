@@ -162,6 +162,7 @@ bool tb_depth_supported(int k) {
 int tb_strip_width(int k) { return 256 - 2 * int(round_up(k, 4)); }
 
 int tb_variant_lag(int variant) {
+  if ((variant & 3) == 3 && (variant & 8)) return 4;  // ramp + 6-row prefetch
   switch (variant & 3) {
     case 1: return 2;
     case 2: return 0;

@@ -116,10 +116,12 @@ struct TbStream {
   static constexpr bool ROWCHK = MODE == kModeGeneric;
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
   static constexpr int RING = LAG == 0 ? 2 : (LAG == 2 ? 4 : 3);
+  // Prefetch distance in rows (LAG 4 = LAG 3 with a 6-row prefetch ring).
+  static constexpr int PF = LAG == 4 ? 6 : RING;
   static constexpr int SKEW = LAG == 2 ? 2 : 1;
   static constexpr int STEP = LAG == 2 ? 2 : 1;  // row skew per level in the ring bodies
   float4 R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
-  float4 P[RING];     // prefetch ring (input row i + RING)
+  float4 P[PF];       // prefetch ring (input row i + PF)
   unsigned m = 0;
 
   __device__ __forceinline__ void emit(const float4& out, const float4& b, int64_t ro,
@@ -136,7 +138,7 @@ struct TbStream {
     }
   }
 
-  template <int U>
+  template <int U, int V = U>
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int rlo, int rhi,
@@ -163,10 +165,10 @@ struct TbStream {
         c = cn;
       }
     } else {
-      R[0][U] = P[U];
+      R[0][U] = P[V];
       {
-        const int64_t nxt = min(i + RING, last_in);
-        P[U] = *reinterpret_cast<const float4*>(src + nxt * pitch);
+        const int64_t nxt = min(i + PF, last_in);
+        P[V] = *reinterpret_cast<const float4*>(src + nxt * pitch);
       }
       // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
       // iterations, so the order below carries no dependency.
@@ -205,10 +207,10 @@ struct TbStream {
                                        int64_t pitch, int64_t last_in, int rlo, int rhi,
                                        const RowUpdate<MODE>& upd) {
     if constexpr (T < 2 * K) {
-      constexpr int U = T % 3;
+      constexpr int U = T % 3, V = T % PF;
       const int64_t i = first_in + T;
-      R[0][U] = P[U];
-      P[U] = *reinterpret_cast<const float4*>(src + min(i + 3, last_in) * pitch);
+      R[0][U] = P[V];
+      P[V] = *reinterpret_cast<const float4*>(src + min(i + PF, last_in) * pitch);
       ramp_levels<T, 1>(i, rlo, rhi, upd);
       __builtin_amdgcn_sched_barrier(0);
       ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -228,8 +230,29 @@ struct TbStream {
 #pragma unroll
       for (int j = 0; j < RING; ++j) R[s][j] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < RING; ++j)
+    for (int j = 0; j < PF; ++j)
       P[j] = *reinterpret_cast<const float4*>(src + min(first_in + j, last_in) * pitch);
+    if constexpr (LAG == 4) {
+      // As LAG 3, with the main loop unrolled by 6 for the 6-row prefetch ring.
+      ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
+      constexpr int T0 = 2 * K;
+      for (int64_t t = T0; t < T; t += 6) {
+        const int64_t i = first_in + t;
+        body<(T0 + 0) % 3, (T0 + 0) % 6>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                         store_lane, upd, want_resid);
+        body<(T0 + 1) % 3, (T0 + 1) % 6>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo,
+                                         rhi, store_lane, upd, want_resid);
+        body<(T0 + 2) % 3, (T0 + 2) % 6>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo,
+                                         rhi, store_lane, upd, want_resid);
+        body<(T0 + 3) % 3, (T0 + 3) % 6>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo,
+                                         rhi, store_lane, upd, want_resid);
+        body<(T0 + 4) % 3, (T0 + 4) % 6>(i + 4, t + 4, src, dst, pitch, last_in, rb, re, rlo,
+                                         rhi, store_lane, upd, want_resid);
+        body<(T0 + 5) % 3, (T0 + 5) % 6>(i + 5, t + 5, src, dst, pitch, last_in, rb, re, rlo,
+                                         rhi, store_lane, upd, want_resid);
+      }
+      return;
+    }
     if constexpr (LAG == 3) {
       // Pipeline ramp: during iteration t < 2K only levels s <= t/2 compute
       // rows the chunk's output trapezoid needs; a plain loop would compute
@@ -267,6 +290,7 @@ struct TbStream {
 template <int K, int LAG>
 constexpr int tb_waves_per_simd() {
   if (LAG == 2) return K <= 4 ? 4 : 2;
+  if (LAG == 4) return K <= 2 ? 6 : K <= 4 ? 4 : K <= 6 ? 3 : K <= 8 ? 3 : 2;
   return K <= 2 ? 6 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 8 ? 3 : 2;
 }
 
@@ -394,7 +418,10 @@ int occupancy(int depth, int lag) {
   }
 }
 
-// Returns false if (depth, lag) is not instantiated.  Only the skew-1
+// Returns false if (depth, lag) is not instantiated.  LAG 4 (6-row prefetch)
+// measured equal to LAG 3 (profiles/tb_depth_bandwidth_calibration_r1.jsonl:
+// K=8 already moves ~4.4 TB/s of the ~4.9 TB/s this access pattern reaches)
+// and is not instantiated either.  Only the skew-1
 // pipelines (LAG 1, and LAG 3 = LAG 1 + ramp) are instantiated: the skew-2
 // (LAG 2) and 2-slot (LAG 0) forms lost every sweep (profiles/tb_sweep_*.json)
 // and only cost build time.

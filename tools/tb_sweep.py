@@ -72,7 +72,7 @@ def main():
     for c in combos:
         v, k, w = c
         med = statistics.median(res[c])
-        rows.append({"variant": v, "pipe": ["ring3", "ring4", "ring2", "ring3ramp"][v & 3], "build": "scalar" if v & 4 else "packed",
+        rows.append({"variant": v, "pipe": (["ring3", "ring4", "ring2", "ring3ramp"][v & 3] + ("+pf6" if v & 8 else "")), "build": "scalar" if v & 4 else "packed",
                      "depth": k, "waves": w, "gcells_s": round(med, 1),
                      "min": round(min(res[c]), 1), "max": round(max(res[c]), 1),
                      "nx": nx, "ny": n,
