@@ -42,6 +42,10 @@ $(LIBDIR)/libheat.so: $(OBJS)
 $(BUILD)/heat: csrc/apps/heat_main.cpp $(OBJS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip csrc/apps/heat_main.cpp -x none $(OBJS) -o $@ $(LDFLAGS)
 
+probe: $(BUILD)/overlap_probe
+$(BUILD)/overlap_probe: tools/overlap_probe.cpp $(OBJS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -x hip tools/overlap_probe.cpp -x none $(OBJS) -o $@ $(LDFLAGS)
+
 asm: $(SRCS_HIP)
 	@mkdir -p $(BUILD)/asm
 	cd $(BUILD)/asm && for f in $(SRCS_HIP); do \

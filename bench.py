@@ -121,7 +121,8 @@ def main() -> int:
                 "seq_len": args.nx * args.ny,
                 "iters_per_step": args.iters_per_step,
                 "parallelism": f"domain-decomp {solver.info.px}x{solver.info.py} "
-                               f"({solver.transport}), tb_depth {solver.info.tb_depth}",
+                               f"({solver.transport}), tb_depth {solver.info.tb_depth}, "
+                               f"halo {solver.info.halo}, schedule {solver.info.schedule}",
                 "converge_check": bool(args.converge),
             },
         }

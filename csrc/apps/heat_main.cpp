@@ -47,6 +47,8 @@ void usage() {
       "  --dump-initial          also write the initial grid\n"
       "  --compat none|mpi|cuda  reference step-count/check semantics   [none]\n"
       "  --no-graph --no-overlap disable hipGraph capture / comm overlap\n"
+      "  --schedule auto|sync|overlap|pipeline   multi-rank pass schedule [auto=sync]\n"
+      "  --halo-passes M         sync schedule: passes per halo exchange [auto]\n"
       "  --checkpoint PATH --checkpoint-every K   periodic binary checkpoints\n"
       "  --resume PATH           start from a binary checkpoint\n"
       "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
@@ -123,6 +125,13 @@ int main(int argc, char** argv) {
     else if (a == "--graph") P.use_graph = true;
     else if (a == "--no-overlap") P.overlap = false;
     else if (a == "--overlap") P.overlap = true;
+    else if (a == "--schedule") {
+      std::string s = need();
+      P.schedule = s == "sync"       ? Schedule::Sync
+                   : s == "overlap"  ? Schedule::Overlap
+                   : s == "pipeline" ? Schedule::Pipeline
+                                     : Schedule::Auto;
+    } else if (a == "--halo-passes") P.halo_passes = std::atoi(need().c_str());
     else if (a == "--checkpoint") checkpoint = need();
     else if (a == "--checkpoint-every") ckpt_every = std::atoll(need().c_str());
     else if (a == "--resume") resume = need();

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define HEAT_ABI_VERSION 1
+#define HEAT_ABI_VERSION 2
 
 typedef struct heat_params {
   int64_t nx, ny;
@@ -35,6 +35,8 @@ typedef struct heat_params {
   int32_t use_graph, overlap;
   int32_t compat;    /* 0 none, 1 mpi, 2 cuda */
   int32_t device;
+  int32_t schedule;    /* 0 auto, 1 sync, 2 overlap (exchange-first), 3 pipeline */
+  int32_t halo_passes; /* sync schedule: passes per exchange (0 = auto) */
 } heat_params;
 
 /* Transport selection for heat_solver_create. */
@@ -68,6 +70,8 @@ typedef struct heat_block_info {
   int64_t pitch, rows;
   int32_t hx, hy, halo, tb_depth;
   int64_t bytes_per_field;
+  int32_t schedule; /* effective heat::Schedule (1 sync, 2 overlap, 3 pipeline) */
+  int32_t pad_;
 } heat_block_info;
 
 typedef struct heat_checksum {

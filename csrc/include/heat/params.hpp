@@ -45,6 +45,21 @@ enum class DecompKind : int {
   Grid2D = 2,
 };
 
+// Pass schedule of a multi-rank GPU run (the reference overlaps
+// inner-cell compute with MPI_Isend/Irecv).  Measured on MI355X
+// (profiles/overlap_probe_r1.md): cross-queue event hops cost ~10 us and
+// the boundary bands of a K=8 pass are a latency-bound ~10 us launch, more
+// than a 1024x8192 slab's exchange saves by overlapping, so the default is
+// the deep-halo synchronous schedule, which instead exchanges m*K-deep
+// ghosts once per m passes and computes the shrinking ghost region
+// redundantly (one launch per pass, one exchange per m passes).
+enum class Schedule : int {
+  Auto = 0,      // Sync
+  Sync = 1,      // exchange (when ghosts run out) then one launch per pass
+  Overlap = 2,   // exchange-first: exchange || interior, then boundary bands
+  Pipeline = 3,  // boundary-first: bands, then next exchange || interior
+};
+
 struct Params {
   int64_t nx = 20;  // rows (slow index), NXPROB
   int64_t ny = 20;  // columns (contiguous index), NYPROB
@@ -65,10 +80,13 @@ struct Params {
   bool overlap = true;      // halo exchange concurrent with interior compute
   Compat compat = Compat::None;
   int device = -1;          // HIP device ordinal (-1 = local rank % device count)
+  Schedule schedule = Schedule::Auto;
+  int halo_passes = 0;      // passes per exchange with Sync (ghost depth m*K); 0 = auto
 };
 
 const char* init_mode_name(InitMode m);
 const char* kernel_name(KernelKind k);
 const char* compat_name(Compat c);
+const char* schedule_name(Schedule s);
 
 }  // namespace heat

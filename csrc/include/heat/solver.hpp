@@ -9,13 +9,15 @@
 //   gather + output              mpi/...c:270-299, cuda/cuda_heat.cu:242-251          (R19)
 //
 // MI355X-first execution model:
-//   * A "pass" advances k steps: exchange a k-deep halo (RCCL, grouped), then
-//     one temporally blocked kernel computes all k steps.  k = tb depth, so
-//     there is one exchange per k steps (communication avoiding) instead of
-//     one per step as in the reference.
-//   * With overlap on, the interior box (whose dependency cone does not
-//     reach the ghost ring) runs on the compute stream while the exchange
-//     runs on the comm stream; the boundary boxes follow after an event join.
+//   * A "pass" advances k steps with one temporally blocked launch (k = tb
+//     depth).  Ghosts are H = m*k deep: one exchange (RCCL, grouped) feeds m
+//     passes, each of which also recomputes the still-valid part of the ghost
+//     ring (communication avoiding: one exchange per m*k steps instead of one
+//     per step as in the reference).
+//   * Alternative schedules (Params::schedule) overlap the exchange with the
+//     interior box on a high-priority comm stream: exchange-first or
+//     boundary-first.  Measured slower on MI355X at the strong-scaling shapes
+//     (see params.hpp), kept selectable and tested.
 //   * Segments between convergence checks are captured once into a hipGraph
 //     per (length, parity) and replayed.
 #pragma once
@@ -25,6 +27,7 @@
 #include <map>
 #include <memory>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "heat/io.hpp"
@@ -67,6 +70,7 @@ class Solver {
   Transport& transport() { return *tr_; }
   int64_t step() const { return step_; }
   int halo() const { return H_; }
+  Schedule schedule() const { return sched_; }
   int tb_depth() const { return T_; }
   bool on_gpu() const { return P_.backend == Backend::Hip; }
 
@@ -102,8 +106,10 @@ class Solver {
   void enqueue_segment(int64_t n, bool resid);
   void enqueue_pass(int k, bool resid);
   void exchange(int buf, int k, hipStream_t st);
-  void compute_gpu(int k, bool resid, bool split, int part);
-  void compute_cpu(int k, bool resid);
+  void compute_gpu(int k, bool resid, bool split, int part, int band = 0, int64_t er = 0,
+                   int64_t ec = 0);
+  void compute_cpu(int k, bool resid, int64_t er, int64_t ec);
+  std::pair<int64_t, int64_t> ensure_ghosts(int k, hipStream_t st);
   float finish_resid();
   bool is_check_point(int64_t completed) const;
   bool converged_value(float r) const;
@@ -114,9 +120,13 @@ class Solver {
   Cart cart_;
   Block blk_;
   Layout L_;
-  int H_ = 1;  // ghost depth (max pass depth)
+  int H_ = 1;  // ghost depth: m * T (m passes per exchange)
   int T_ = 1;  // pass depth (TB depth on the GPU)
+  Schedule sched_ = Schedule::Sync;
   bool staged_ = false;  // GPU fields but host-memory transport
+  bool warmed_ = false;    // RCCL connections established outside capture
+  int64_t gr_ = 0, gc_ = 0;  // ghost rows/columns of field_[cur_] at the current level
+  bool comm_pending_ = false;  // comm stream has unjoined work
   int cur_ = 0;
   int64_t step_ = 0;
   int64_t resid_pending_ = 0;
@@ -142,9 +152,10 @@ class Solver {
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
     int cur_after = 0;
+    int64_t gr_after = 0, gc_after = 0;
     int64_t passes = 0, exchanges = 0;
   };
-  std::map<std::tuple<int64_t, bool, int>, GraphEntry> graphs_;
+  std::map<std::tuple<int64_t, bool, int, int64_t, int64_t>, GraphEntry> graphs_;
   bool capturing_ = false;
 };
 

@@ -123,6 +123,7 @@ struct TbStream {
   float4 R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
   float4 P[PF];       // prefetch ring (input row i + PF)
   unsigned m = 0;
+  int rc = 4;  // elements of this lane inside the box (the residual skips the rest)
 
   __device__ __forceinline__ void emit(const float4& out, const float4& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
@@ -130,10 +131,12 @@ struct TbStream {
     if (ro >= rb && ro < re && store_lane) {
       *reinterpret_cast<float4*>(dst + ro * pitch) = out;
       if (want_resid) {
+        // Columns past the box end (the last lane's spill into padding or
+        // stale ghost columns) are written but not part of the residual.
         m = max(m, __float_as_uint(fabsf(out.x - b.x)));
-        m = max(m, __float_as_uint(fabsf(out.y - b.y)));
-        m = max(m, __float_as_uint(fabsf(out.z - b.z)));
-        m = max(m, __float_as_uint(fabsf(out.w - b.w)));
+        m = max(m, rc > 1 ? __float_as_uint(fabsf(out.y - b.y)) : 0u);
+        m = max(m, rc > 2 ? __float_as_uint(fabsf(out.z - b.z)) : 0u);
+        m = max(m, rc > 3 ? __float_as_uint(fabsf(out.w - b.w)) : 0u);
       }
     }
   }
@@ -352,6 +355,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
       upd.cm0 = gy <= g.ny - 1 && g.ny - 1 < gy + 4;  // this lane holds column ny-1
     }
     TbStream<K, LAG, MD> st;
+    st.rc = int(min<int64_t>(cend - col, 4));
     st.run(src, dst, g.pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
     m = st.m;
   };

@@ -42,6 +42,16 @@ const char* compat_name(Compat c) {
   return "?";
 }
 
+const char* schedule_name(Schedule s) {
+  switch (s) {
+    case Schedule::Auto: return "auto";
+    case Schedule::Sync: return "sync";
+    case Schedule::Overlap: return "overlap";
+    case Schedule::Pipeline: return "pipeline";
+  }
+  return "?";
+}
+
 Params params_from_c(const heat_params* p) {
   Params P;
   P.nx = p->nx;
@@ -64,6 +74,8 @@ Params params_from_c(const heat_params* p) {
   P.overlap = p->overlap != 0;
   P.compat = Compat(p->compat);
   P.device = p->device;
+  P.schedule = Schedule(p->schedule);
+  P.halo_passes = p->halo_passes;
   return P;
 }
 
@@ -213,6 +225,8 @@ int heat_solver_info(heat_solver* s, heat_block_info* o) {
     o->halo = s->s->halo();
     o->tb_depth = s->s->tb_depth();
     o->bytes_per_field = L.bytes();
+    o->schedule = int32_t(s->s->schedule());
+    o->pad_ = 0;
   });
 }
 

@@ -49,21 +49,44 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
       T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 8);
       HEAT_CHECK(gpu::tb_depth_supported(T_), "TB depth %d not supported", T_);
     }
-    HEAT_CHECK(!(tr_->device_memory() && tr_->world() > 1) || true, "");
   } else {
     HEAT_CHECK(!tr_->device_memory(), "transport %s needs the GPU backend", tr_->name());
     T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
     cpu::set_threads(P_.threads);
   }
-  H_ = T_;
+  // Every decision below is made from global quantities (the smallest block
+  // of any rank), so all ranks take the same path and their exchanges match.
+  const int world = tr_->world();
+  int64_t min_lx = blk_.lx, min_ly = blk_.ly;
+  for (int r = 0; r < cart_.world; ++r) {
+    const Block b = make_block(cart_, r, P_.nx, P_.ny);
+    min_lx = std::min(min_lx, b.lx);
+    min_ly = std::min(min_ly, b.ly);
+  }
+  const int64_t min_ext = std::min(cart_.px > 1 ? min_lx : INT64_MAX, cart_.py > 1 ? min_ly : INT64_MAX);
+  sched_ = P_.schedule == Schedule::Auto ? Schedule::Sync : P_.schedule;
+  if (!on_gpu() || P_.kernel == KernelKind::Naive || world == 1 || !P_.overlap)
+    sched_ = Schedule::Sync;
+  // Ghost depth H = m*T: with the Sync schedule one exchange feeds m passes,
+  // each computing the still-valid part of the ghost ring redundantly.
+  int m = 1;
+  if (sched_ == Schedule::Sync && world > 1) {
+    m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 4) : 1);
+    m = int(std::max<int64_t>(1, std::min<int64_t>(m, min_ext / T_)));
+  }
+  H_ = m * T_;
   // A rank must own at least H rows/columns along every decomposed axis so
-  // that a k-deep halo comes from its direct neighbour only.
+  // that an H-deep halo comes from its direct neighbour only.
   HEAT_CHECK(cart_.px == 1 || blk_.lx >= H_, "block of %lld rows is thinner than halo depth %d",
              (long long)blk_.lx, H_);
   HEAT_CHECK(cart_.py == 1 || blk_.ly >= H_, "block of %lld cols is thinner than halo depth %d",
              (long long)blk_.ly, H_);
+  // The boundary-first pipeline needs an interior box off H-deep bands.
+  if (sched_ == Schedule::Pipeline &&
+      !(min_lx > 2 * int64_t(H_) && round_down(min_ly - H_, 4) > round_up(H_, 4)))
+    sched_ = Schedule::Sync;
   L_ = Layout::make(blk_.lx, blk_.ly, H_);
-  staged_ = on_gpu() && !tr_->device_memory() && tr_->world() > 1;
+  staged_ = on_gpu() && !tr_->device_memory() && world > 1;
   alloc();
   init_fields();
 }
@@ -82,7 +105,13 @@ void Solver::alloc() {
     if (cart_.py > 1)
       for (auto& b : ew_) HIP_CHECK(hipMalloc(&b, ew_elems * 4));
     HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+    {
+      // The comm stream gets the highest priority so RCCL's kernels are
+      // dispatched ahead of queued stencil workgroups.
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, greatest));
+    }
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreate(&ev_t0_));
@@ -154,6 +183,7 @@ void Solver::init_fields() {
   if (on_gpu()) HIP_CHECK(hipStreamSynchronize(s_comp_));
   cur_ = 0;
   step_ = 0;
+  gr_ = gc_ = 0;
 }
 
 void Solver::reset() { init_fields(); }
@@ -252,7 +282,8 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // compute
 // ---------------------------------------------------------------------------
-void Solver::compute_gpu(int k, bool resid, bool split, int part) {
+void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int64_t er,
+                         int64_t ec) {
   const float* src = field_[cur_];
   float* dst = field_[cur_ ^ 1];
   gpu::StencilGeom g;
@@ -267,13 +298,17 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part) {
   const int64_t lx = blk_.lx, ly = blk_.ly;
   const auto& nb = blk_.nbr;
   static const int waves_target = env_int("HEAT_TB_WAVES", 0);
+  // The box of this pass: the owned block grown by (er, ec) into the ghost
+  // ring on sides that have a neighbour (deep-halo passes).
+  const Box own{nb[North] >= 0 ? -er : 0, lx + (nb[South] >= 0 ? er : 0),
+                nb[West] >= 0 ? -ec : 0, ly + (nb[East] >= 0 ? ec : 0)};
 
   if (P_.kernel == KernelKind::Naive) {
     // k single steps over shrinking regions (deep halo), ping-ponging.
     for (int j = 0; j < k; ++j) {
       const int64_t e = k - 1 - j;
-      Box b{nb[North] >= 0 ? -e : 0, lx + (nb[South] >= 0 ? e : 0), nb[West] >= 0 ? -e : 0,
-            ly + (nb[East] >= 0 ? e : 0)};
+      Box b{nb[North] >= 0 ? own.r0 - e : 0, own.r1 + (nb[South] >= 0 ? e : 0),
+            nb[West] >= 0 ? own.c0 - e : 0, own.c1 + (nb[East] >= 0 ? e : 0)};
       const float* a = field_[cur_];
       float* d = field_[cur_ ^ 1];
       gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
@@ -283,13 +318,16 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part) {
   }
 
   if (!split) {
-    Box full{0, lx, 0, ly};
-    gpu::tb_step(src, dst, g, &full, 1, k, r, s_comp_, waves_target);
+    gpu::tb_step(src, dst, g, &own, 1, k, r, s_comp_, waves_target);
     return;
   }
-  const int64_t r0 = nb[North] >= 0 ? k : 0, r1 = nb[South] >= 0 ? lx - k : lx;
-  const int64_t c0 = nb[West] >= 0 ? round_up(k, 4) : 0;
-  const int64_t c1 = nb[East] >= 0 ? round_down(ly - k, 4) : ly;
+  // Boundary bands are `band` >= k deep (k for exchange-first; H for the
+  // boundary-first pipeline, whose next exchange sends H rows/columns that
+  // the concurrent interior launch must not write).
+  if (band < k) band = k;
+  const int64_t r0 = nb[North] >= 0 ? band : 0, r1 = nb[South] >= 0 ? lx - band : lx;
+  const int64_t c0 = nb[West] >= 0 ? round_up(band, 4) : 0;
+  const int64_t c1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
   if (part == 0) {
     Box in{r0, r1, c0, c1};
     gpu::tb_step(src, dst, g, &in, 1, k, r, s_comp_, waves_target);
@@ -300,7 +338,7 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part) {
   }
 }
 
-void Solver::compute_cpu(int k, bool resid) {
+void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
   cpu::Geom g;
   g.pitch = L_.pitch;
   g.gx0 = blk_.ox;
@@ -312,8 +350,8 @@ void Solver::compute_cpu(int k, bool resid) {
   const auto& nb = blk_.nbr;
   for (int j = 0; j < k; ++j) {
     const int64_t e = k - 1 - j;
-    Box b{nb[North] >= 0 ? -e : 0, blk_.lx + (nb[South] >= 0 ? e : 0), nb[West] >= 0 ? -e : 0,
-          blk_.ly + (nb[East] >= 0 ? e : 0)};
+    Box b{nb[North] >= 0 ? -(er + e) : 0, blk_.lx + (nb[South] >= 0 ? er + e : 0),
+          nb[West] >= 0 ? -(ec + e) : 0, blk_.ly + (nb[East] >= 0 ? ec + e : 0)};
     const bool last = j == k - 1;
     float r = cpu::step(field_[cur_], field_[cur_ ^ 1], g, b, resid && last);
     if (resid && last) cpu_resid_ = r;
@@ -321,20 +359,71 @@ void Solver::compute_cpu(int k, bool resid) {
   }
 }
 
+std::pair<int64_t, int64_t> Solver::ensure_ghosts(int k, hipStream_t st) {
+  // gr_/gc_: how many ghost rows/columns of field_[cur_] hold the current
+  // time level.  A k-step pass needs k; an exchange refills H.  The pass
+  // then also updates the (valid - k) ghost rows/columns next to the block,
+  // which become the valid ghosts of the next level.  Only axes that are
+  // decomposed count, so every rank makes the same decision.
+  const bool ns = cart_.px > 1, ew = cart_.py > 1;
+  if ((ns && gr_ < k) || (ew && gc_ < k)) {
+    exchange(cur_, H_, st);
+    gr_ = gc_ = H_;
+  }
+  // TB boxes start on a float4 column: round the column extension down.
+  const bool tb = on_gpu() && P_.kernel != KernelKind::Naive;
+  const int64_t er = ns ? gr_ - k : 0;
+  const int64_t ec = ew ? (tb ? round_down(gc_ - k, 4) : gc_ - k) : 0;
+  gr_ = er;
+  gc_ = ec;
+  return {er, ec};
+}
+
 void Solver::enqueue_pass(int k, bool resid) {
   const auto& nb = blk_.nbr;
-  const bool has_nbr = nb[0] >= 0 || nb[1] >= 0 || nb[2] >= 0 || nb[3] >= 0;
+  // With world > 1 every rank of the (non-periodic) grid has a neighbour.
+  const bool multi = tr_->world() > 1;
   if (on_gpu()) {
     if (resid) HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
     const bool tb = P_.kernel != KernelKind::Naive;
     const int64_t lx = blk_.lx, ly = blk_.ly;
-    const int64_t ir0 = nb[North] >= 0 ? k : 0, ir1 = nb[South] >= 0 ? lx - k : lx;
-    const int64_t ic0 = nb[West] >= 0 ? round_up(k, 4) : 0;
-    const int64_t ic1 = nb[East] >= 0 ? round_down(ly - k, 4) : ly;
+    const int band = sched_ == Schedule::Pipeline ? H_ : k;
+    const int64_t ir0 = nb[North] >= 0 ? band : 0, ir1 = nb[South] >= 0 ? lx - band : lx;
+    const int64_t ic0 = nb[West] >= 0 ? round_up(band, 4) : 0;
+    const int64_t ic1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
     const bool interior_ok = ir1 > ir0 && ic1 > ic0;
-    if (!has_nbr) {
+    if (!multi) {
       compute_gpu(k, resid, false, 0);
-    } else if (tb && P_.overlap && !staged_ && interior_ok) {
+    } else if (sched_ == Schedule::Pipeline) {
+      // Boundary-first: the H-deep ghosts of cur_ were exchanged by the
+      // previous pass (or now, if stale).  Compute the H-deep boundary bands,
+      // then post the NEXT pass's exchange (its send rows/columns all lie in
+      // the bands) on the high-priority comm stream, concurrent with the
+      // interior launch.
+      if (gr_ < H_ || gc_ < H_) {
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+        exchange(cur_, H_, s_comm_);
+        HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+        comm_pending_ = true;
+      }
+      // Only wait on an exchange posted in this segment: a segment ends by
+      // joining the comm stream, and a captured graph may not wait on an
+      // event recorded outside its capture.
+      if (comm_pending_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+      compute_gpu(k, resid, true, 1, band);
+      HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+      // The interior is enqueued before the exchange: the stream semantics
+      // are the same (s_comm waits for the bands only), and a host-staged
+      // exchange, which blocks the host, then overlaps the interior too.
+      compute_gpu(k, resid, true, 0, band);
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+      exchange(cur_ ^ 1, H_, s_comm_);
+      HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+      comm_pending_ = true;
+      gr_ = gc_ = H_;  // for the buffer that becomes cur_ below
+    } else if (sched_ == Schedule::Overlap && tb && interior_ok) {
+      // Exchange-first: exchange || interior, then the boundary bands.
       HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
       exchange(cur_, k, s_comm_);
@@ -342,9 +431,15 @@ void Solver::enqueue_pass(int k, bool resid) {
       compute_gpu(k, resid, true, 0);
       HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
       compute_gpu(k, resid, true, 1);
-    } else {
+      gr_ = gc_ = 0;
+    } else if (sched_ == Schedule::Overlap) {
       exchange(cur_, k, s_comp_);
       compute_gpu(k, resid, false, 0);
+      gr_ = gc_ = 0;
+    } else {
+      // Sync (default): one launch per pass, one exchange per H/k passes.
+      const auto ext = ensure_ghosts(k, s_comp_);
+      compute_gpu(k, resid, false, 0, 0, ext.first, ext.second);
     }
     if (tb) cur_ ^= 1;
     if (resid) {
@@ -352,8 +447,9 @@ void Solver::enqueue_pass(int k, bool resid) {
       HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
     }
   } else {
-    if (has_nbr) exchange(cur_, k, nullptr);
-    compute_cpu(k, resid);
+    std::pair<int64_t, int64_t> ext{0, 0};
+    if (multi) ext = ensure_ghosts(k, nullptr);
+    compute_cpu(k, resid, ext.first, ext.second);
   }
   step_ += k;
   ++stat_passes_;
@@ -362,6 +458,13 @@ void Solver::enqueue_pass(int k, bool resid) {
 void Solver::enqueue_segment(int64_t n, bool resid) {
   auto d = pass_depths(n);
   for (size_t i = 0; i < d.size(); ++i) enqueue_pass(d[i], resid && i + 1 == d.size());
+  if (comm_pending_) {
+    // Join the comm stream (the last pass posted the next exchange): a
+    // captured graph must end on its origin stream, and the next segment
+    // relies on those ghosts.
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+    comm_pending_ = false;
+  }
 }
 
 float Solver::finish_resid() {
@@ -400,14 +503,13 @@ RunStats Solver::run(int64_t steps) {
   const bool can_graph = gpu && P_.use_graph && !staged_ &&
                          (tr_->world() == 1 || tr_->graph_capturable()) &&
                          env_int("HEAT_GRAPH", 1) != 0;
-  static bool warmed = false;
-  if (can_graph && tr_->world() > 1 && !warmed) {
+  if (can_graph && tr_->world() > 1 && !warmed_) {
     // Let RCCL establish its connections outside of stream capture.  A halo
     // exchange of the current buffer is idempotent.
     exchange(cur_, H_, s_comp_);
     tr_->allreduce_max(reinterpret_cast<float*>(d_scratch_), 1, s_comp_);
     HIP_CHECK(hipStreamSynchronize(s_comp_));
-    warmed = true;
+    warmed_ = true;
   }
   int64_t remaining = steps;
   while (remaining > 0) {
@@ -425,7 +527,7 @@ RunStats Solver::run(int64_t steps) {
       }
     }
     if (can_graph) {
-      const auto key = std::make_tuple(seg, resid, cur_);
+      const auto key = std::make_tuple(seg, resid, cur_, gr_, gc_);
       auto it = graphs_.find(key);
       const int cur_before = cur_;
       const int64_t step_before = step_;
@@ -449,6 +551,8 @@ RunStats Solver::run(int64_t steps) {
         HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
         HIP_CHECK(hipGraphDestroy(graph));
         e.cur_after = cur_;
+        e.gr_after = gr_;
+        e.gc_after = gc_;
         e.passes = stat_passes_ - p_before;
         e.exchanges = stat_exchanges_ - e_before;
         stat_passes_ = p_before;
@@ -457,6 +561,8 @@ RunStats Solver::run(int64_t steps) {
       }
       HIP_CHECK(hipGraphLaunch(it->second.exec, s_comp_));
       cur_ = it->second.cur_after;
+      gr_ = it->second.gr_after;
+      gc_ = it->second.gc_after;
       step_ = step_before + seg;
       stat_passes_ += it->second.passes;
       stat_exchanges_ += it->second.exchanges;
@@ -525,6 +631,7 @@ void Solver::load_owned(const float* host, int64_t host_pitch, int64_t step) {
   }
   synchronize();
   step_ = step;
+  gr_ = gc_ = 0;
 }
 
 void Solver::scatter_root(const float* full, int64_t step) {

@@ -22,6 +22,8 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be imported before libheat: shared HIP runtime)
 
+ABI_VERSION = 2  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
+
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 LIB_PATH = PKG_DIR / "_lib" / "libheat.so"
@@ -47,6 +49,7 @@ class HeatParams(Structure):
         ("decomp", c_int32), ("px", c_int32), ("py", c_int32),
         ("use_graph", c_int32), ("overlap", c_int32),
         ("compat", c_int32), ("device", c_int32),
+        ("schedule", c_int32), ("halo_passes", c_int32),
     ]
 
 
@@ -88,6 +91,7 @@ class HeatBlockInfo(Structure):
         ("pitch", c_int64), ("rows", c_int64),
         ("hx", c_int32), ("hy", c_int32), ("halo", c_int32), ("tb_depth", c_int32),
         ("bytes_per_field", c_int64),
+        ("schedule", c_int32), ("pad_", c_int32),
     ]
 
 
@@ -180,7 +184,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.heat_abi_version() != 1:
+        if L.heat_abi_version() != ABI_VERSION:
             raise NativeError("libheat ABI mismatch; rebuild with `make`")
         _lib = L
         return _lib

@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--compat", choices=["none", "mpi", "cuda"], default=None)
     a("--no-graph", action="store_true")
     a("--no-overlap", action="store_true")
+    a("--schedule", choices=["auto", "sync", "overlap", "pipeline"], default="auto")
+    a("--halo-passes", type=int, default=0)
     a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
@@ -67,7 +69,8 @@ def main(argv=None) -> int:
                      init=args.init, seed=args.seed, backend=backend, kernel=args.kernel,
                      tb_depth=args.tb_depth, threads=args.threads, decomp=args.decomp,
                      px=args.px, py=args.py, use_graph=not args.no_graph,
-                     overlap=not args.no_overlap, compat=compat)
+                     overlap=not args.no_overlap, compat=compat, schedule=args.schedule,
+                     halo_passes=args.halo_passes)
     info = pcomm.init_distributed("nccl" if backend == "hip" else "gloo")
     root = info.is_root
     out = sys.stdout

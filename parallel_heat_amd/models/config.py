@@ -17,6 +17,7 @@ BACKENDS = {"cpu": 0, "hip": 1}
 KERNELS = {"auto": 0, "naive": 1, "tb": 2}
 DECOMPS = {"auto": 0, "rows": 1, "1d": 1, "2d": 2}
 COMPATS = {"none": 0, "mpi": 1, "cuda": 2}
+SCHEDULES = {"auto": 0, "sync": 1, "overlap": 2, "pipeline": 3}
 
 
 @dataclass
@@ -42,6 +43,8 @@ class HeatConfig:
     overlap: bool = True
     compat: str = "none"          # none | mpi | cuda  
     device: int = -1
+    schedule: str = "auto"        # multi-rank pass schedule: auto(=sync) | sync | overlap | pipeline
+    halo_passes: int = 0          # sync: passes per halo exchange (ghost depth m*K); 0 = auto
 
     def replace(self, **kw) -> "HeatConfig":
         return dataclasses.replace(self, **kw)
@@ -50,11 +53,14 @@ class HeatConfig:
         if self.nx < 1 or self.ny < 1:
             raise ValueError(f"grid {self.nx}x{self.ny}")
         for name, table in (("init", INIT_MODES), ("backend", BACKENDS), ("kernel", KERNELS),
-                            ("decomp", DECOMPS), ("compat", COMPATS)):
+                            ("decomp", DECOMPS), ("compat", COMPATS),
+                            ("schedule", SCHEDULES)):
             if getattr(self, name) not in table:
                 raise ValueError(f"{name}={getattr(self, name)!r}; expected one of {sorted(table)}")
         if self.check_interval < 1:
             raise ValueError("check_interval must be >= 1")
+        if self.halo_passes < 0:
+            raise ValueError("halo_passes must be >= 0")
 
     def total_steps(self) -> int:
         """Updates a full run performs (compat=mpi runs STEPS+1)."""
@@ -80,4 +86,6 @@ class HeatConfig:
         p.overlap = int(bool(self.overlap))
         p.compat = COMPATS[self.compat]
         p.device = int(self.device if device is None else device)
+        p.schedule = SCHEDULES[self.schedule]
+        p.halo_passes = int(self.halo_passes)
         return p

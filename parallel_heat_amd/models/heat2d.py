@@ -72,6 +72,7 @@ class BlockInfo:
     halo: int
     tb_depth: int
     bytes_per_field: int
+    schedule: str
 
 
 class HeatSolver:
@@ -133,7 +134,8 @@ class HeatSolver:
         _native.call("heat_solver_info", self._h, ctypes.byref(i))
         return BlockInfo(i.rank, i.world, i.px, i.py, i.cx, i.cy, i.ox, i.oy, i.lx, i.ly,
                          tuple(i.nbr), i.pitch, i.rows, i.hx, i.hy, i.halo, i.tb_depth,
-                         i.bytes_per_field)
+                         i.bytes_per_field,
+                         {1: "sync", 2: "overlap", 3: "pipeline"}.get(i.schedule, "?"))
 
     @property
     def step(self) -> int:

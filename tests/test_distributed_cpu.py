@@ -31,6 +31,33 @@ def test_invariance_gloo(tmp_path, world, decomp, depth):
     assert np.array_equal(res["grid"], ref)
 
 
+@pytest.mark.parametrize("world,kw", [
+    (2, dict(decomp="rows", tb_depth=2, halo_passes=3)),
+    (2, dict(px=1, py=2, tb_depth=1, halo_passes=4)),
+    (4, dict(decomp="auto", tb_depth=3, halo_passes=2)),
+    (3, dict(decomp="rows", tb_depth=5, halo_passes=9)),   # clamped to the block size
+])
+def test_deep_halo_invariance_gloo(tmp_path, world, kw):
+    # One exchange per halo_passes passes; ghost cells computed redundantly.
+    res = run_world(world, {**BASE, **kw}, 0, tmp_path, chunks=[7, 1, 13, 8])
+    ref, _ = single(BASE, 29)
+    assert np.array_equal(res["grid"], ref)
+    if kw["halo_passes"] <= 4:
+        # The last chunk (8 steps) needs at most ceil(8 / (k*m)) + 1 exchanges.
+        km = kw["tb_depth"] * kw["halo_passes"]
+        assert int(res["exchanges"]) <= -(-8 // km) + 1
+
+
+def test_deep_halo_convergence_gloo(tmp_path):
+    kw = dict(nx=24, ny=30, steps=20000, converge=True, check_interval=20, eps=1e-3,
+              backend="cpu", tb_depth=2, halo_passes=3)
+    res = run_world(4, kw, 20000, tmp_path)
+    ref, r = single(kw, 20000)
+    assert bool(res["conv"]) and r.converged
+    assert int(res["conv_at"]) == r.converged_at
+    assert np.array_equal(res["grid"], ref)
+
+
 def test_invariance_chunked_runs(tmp_path):
     kw = {**BASE, "tb_depth": 3}
     res = run_world(4, kw, 0, tmp_path, chunks=[5, 1, 17])

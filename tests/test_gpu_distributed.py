@@ -1,6 +1,8 @@
-"""Multi-rank GPU paths on ONE MI355X: two ranks share cuda:0 and exchange
-halos through host-staged torch.distributed (gloo).  This runs the real GPU
-kernels, pack/unpack and the staged exchange path under a real decomposition;
+"""Multi-rank GPU paths on ONE MI355X: ranks share cuda:0 and exchange halos
+through host-staged torch.distributed (gloo).  This runs the real GPU kernels,
+pack/unpack and all three pass schedules (sync deep-halo, exchange-first
+overlap, boundary-first pipeline, the overlap ones with the comm stream
+running concurrently with the interior kernel) under a real decomposition;
 results must equal the single-rank GPU run bit for bit."""
 import numpy as np
 import pytest
@@ -11,18 +13,49 @@ from .dist_worker import run_world
 
 pytestmark = pytest.mark.gpu
 
+BASE = dict(nx=150, ny=300, steps=0, init="random", seed=2, backend="hip", tb_depth=8)
 
+
+def single(base, steps):
+    with HeatSolver(HeatConfig(**{**base, "decomp": "auto", "px": 0, "py": 0})) as s:
+        r = s.run(steps)
+        return s.gather(), r
+
+
+@pytest.mark.parametrize("schedule", ["sync", "overlap", "pipeline"])
 @pytest.mark.parametrize("world,kw", [
     (2, dict(decomp="rows")),
     (2, dict(px=1, py=2)),
     (4, dict(decomp="auto")),
     (3, dict(decomp="rows", kernel="naive", tb_depth=2)),
 ])
-def test_gpu_two_ranks_one_device(gpu, tmp_path, world, kw):
-    base = dict(nx=150, ny=300, steps=0, init="random", seed=2, backend="hip", tb_depth=8)
-    base.update(kw)
+def test_gpu_ranks_one_device(gpu, tmp_path, world, kw, schedule):
+    base = {**BASE, **kw, "schedule": schedule}
     res = run_world(world, base, 45, tmp_path, transport="torch")
-    with HeatSolver(HeatConfig(**{**base, "decomp": "auto", "px": 0, "py": 0})) as s:
-        s.run(45)
-        ref = s.gather()
+    ref, _ = single(base, 45)
+    assert np.array_equal(res["grid"], ref)
+
+
+@pytest.mark.parametrize("schedule,m", [("sync", 0), ("sync", 2), ("sync", 1), ("pipeline", 0)])
+def test_gpu_chunked_runs(gpu, tmp_path, schedule, m):
+    # Runs of 5, 1, 17, 22 steps: passes shallower than the halo, ghost
+    # validity carried across run() calls.
+    base = {**BASE, "decomp": "auto", "schedule": schedule, "halo_passes": m}
+    res = run_world(4, base, 0, tmp_path, transport="torch", chunks=[5, 1, 17, 22])
+    ref, _ = single(BASE, 45)
+    assert np.array_equal(res["grid"], ref)
+
+
+@pytest.mark.parametrize("schedule,decomp", [("sync", dict(decomp="rows")),
+                                             ("sync", dict(px=1, py=2)),
+                                             ("pipeline", dict(decomp="rows"))])
+def test_gpu_distributed_convergence(gpu, tmp_path, schedule, decomp):
+    # 2 x (20 x 26) or 2 x (40 x 13) blocks; ny % 4 != 0 so the TB kernel's
+    # last lane spills past the box (excluded from the residual).
+    kw = dict(nx=40, ny=26, steps=40000, converge=True, check_interval=20, eps=1e-3,
+              backend="hip", tb_depth=8, schedule=schedule)
+    res = run_world(2, {**kw, **decomp}, 40000, tmp_path, transport="torch")
+    ref, r = single(kw, 40000)
+    assert bool(res["conv"]) == r.converged
+    assert int(res["conv_at"]) == r.converged_at and int(res["done"]) == r.steps_done
     assert np.array_equal(res["grid"], ref)
