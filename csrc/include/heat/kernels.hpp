@@ -62,10 +62,16 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 int tb_default_variant();
 int tb_variant_lag(int variant);
-// Default whole-rounds of resident waves per launch (HEAT_TB_ROUNDS, default 1).
+// Whole rounds of resident waves per launch (HEAT_TB_ROUNDS; 0 = unset: the
+// planner picks waves per SIMD from the work, tb_auto_waves_per_simd).
 int tb_default_rounds();
 // Resident waves of the TB kernel instantiation on the current device.
 int tb_resident_waves(int depth, int variant);
+// SIMDs of the current device (CUs x 4).
+int tb_simd_count();
+// Waves per SIMD the planner uses for a launch with this much work per SIMD
+// (strip-rows / SIMDs), at most max_per_simd.
+int tb_auto_waves_per_simd(int depth, int64_t strip_rows_per_simd, int max_per_simd);
 
 // Copy a box of a strided field to/from a contiguous buffer (E/W halos).
 void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hipStream_t st);

@@ -174,9 +174,34 @@ int tb_variant_lag(int variant) {
 int tb_default_rounds() {
   static const int r = [] {
     const char* e = std::getenv("HEAT_TB_ROUNDS");
-    return e && *e ? std::max(1, std::atoi(e)) : 1;
+    return e && *e ? std::max(1, std::atoi(e)) : 0;
   }();
   return r;
+}
+
+int tb_simd_count() {
+  static std::map<int, int> cache;
+  static std::mutex mu;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return cache.emplace(dev, std::max(1, cus) * 4).first->second;
+}
+
+int tb_auto_waves_per_simd(int depth, int64_t strip_rows_per_simd, int max_per_simd) {
+  // Fewer, longer chunks for small problems: each chunk pays a ~2K-row
+  // pipeline ramp, and more waves per SIMD only buy latency hiding.  The
+  // thresholds come from the waves sweep over slab heights 512..8192
+  // (tools/sweep_waves.sh, profiles/tb_waves_per_simd_r1.md): at K=8 one
+  // wave per SIMD wins below ~48 strip-rows per SIMD, two below ~100.
+  int w = max_per_simd;
+  if (strip_rows_per_simd < 6 * int64_t(depth)) w = 1;
+  else if (strip_rows_per_simd * 2 < 25 * int64_t(depth)) w = 2;
+  return std::max(1, std::min(w, max_per_simd));
 }
 
 int tb_resident_waves(int depth, int variant) {
@@ -229,13 +254,24 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   if (variant < 0) variant = tb_default_variant();
   const int lag = tb_variant_lag(variant);
-  if (waves_target <= 0) {
-    // Whole rounds of the resident wave capacity: a partial last round leaves
-    // SIMDs idle for the tail of the launch.
-    const int rounds = waves_target < 0 ? -waves_target : tb_default_rounds();
-    waves_target = rounds * tb_resident_waves(depth, variant);
-  }
   const int W = tb_strip_width(depth);
+  int64_t total_strip_rows = 0;
+  for (int b = 0; b < nbox; ++b)
+    if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
+  if (waves_target <= 0) {
+    // Whole rounds of the resident wave capacity (a partial last round leaves
+    // SIMDs idle for the tail of the launch); by default with the number of
+    // waves per SIMD chosen from the work per SIMD.
+    const int resident = tb_resident_waves(depth, variant);
+    const int rounds = waves_target < 0 ? -waves_target : tb_default_rounds();
+    if (rounds > 0) {
+      waves_target = rounds * resident;
+    } else {
+      const int simds = tb_simd_count();
+      waves_target = simds * tb_auto_waves_per_simd(depth, total_strip_rows / simds,
+                                                    std::max(1, resident / simds));
+    }
+  }
   TbArgs args{};
   args.src = src;
   args.dst = dst;
@@ -244,9 +280,6 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   // Split rows into chunks so the whole launch has about waves_target waves,
   // but never shorter than 4*depth rows (keeps the redundant 2*depth-row
   // halo reads below ~50 %).
-  int64_t total_strip_rows = 0;
-  for (int b = 0; b < nbox; ++b)
-    if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
   // Minimum chunk length in rows (multiples of depth; HEAT_TB_MINLEN overrides).
   const char* ml = std::getenv("HEAT_TB_MINLEN");
   const int64_t min_len = ml && *ml ? std::max(1, std::atoi(ml)) : std::max<int64_t>(depth, 8);
