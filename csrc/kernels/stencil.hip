@@ -226,7 +226,8 @@ int tb_resident_waves(int depth, int variant) {
 int tb_default_variant() {
   static const int v = [] {
     const char* e = std::getenv("HEAT_TB_VARIANT");
-    return e && *e ? std::atoi(e) : 7;  // ring-3 + ramp skip, scalar build (tools/tb_sweep.py)
+    // ring-3 + ramp skip, scalar build, XCD-grouped blocks (tools/tb_sweep.py)
+    return e && *e ? std::atoi(e) : 23;
   }();
   return v;
 }
@@ -277,6 +278,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.dst = dst;
   args.resid = resid;
   args.g = g;
+  args.flags = ((variant & 16) ? tbdetail::kTbXcdGroups : 0) |
+               ((variant & 32) ? tbdetail::kTbAltDirection : 0);
   // Split rows into chunks so the whole launch has about waves_target waves,
   // but never shorter than 4*depth rows (keeps the redundant 2*depth-row
   // halo reads below ~50 %).

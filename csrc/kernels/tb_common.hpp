@@ -23,8 +23,19 @@ struct TbArgs {
   unsigned* resid;
   StencilGeom g;
   int nbox, total_waves;
+  int flags;  // kTbXcdGroups | kTbAltDirection
   TbBox box[kMaxBoxes];
 };
+
+// Launch-time layout options (variant bits 16 and 32, see tb_step):
+//   kTbXcdGroups     remap blocks so each XCD (blocks b, b+8, ... under the
+//                    observed round-robin placement) gets a contiguous range
+//                    of waves: vertically adjacent chunks share one L2.
+//   kTbAltDirection  odd chunks stream bottom-up, so the 2K halo rows two
+//                    adjacent chunks both read are read at about the same
+//                    time (both at the start or both at the end).
+constexpr int kTbXcdGroups = 1;
+constexpr int kTbAltDirection = 2;
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
 

@@ -302,7 +302,12 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   constexpr int KK = (K + 3) & ~3;
   constexpr int W = 256 - 2 * KK;
   const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int blk = blockIdx.x;
+  if (a.flags & tbdetail::kTbXcdGroups) {
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = blk & 7, j = blk >> 3;
+    blk = x * q + min(x, r) + j;
+  }
+  const int wave = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave >= a.total_waves) return;
   int bi = 0;
 #pragma unroll
@@ -321,6 +326,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   const StencilGeom& g = a.g;
   const float* src = a.src + col;
   float* dst = a.dst + col;
+  int64_t pitch = g.pitch;
   const bool want_resid = a.resid != nullptr;
 
   // Wave-uniform fast path: every row and column the wave touches is a
@@ -328,8 +334,19 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
   const int64_t gx_lo = g.gx0 + rb - K, gx_hi = g.gx0 + re + K - 1;
   // Updatable local rows (global 1..nx-2), clamped into int32.
-  const int rlo = int(max<int64_t>(1 - g.gx0, -(int64_t(1) << 30)));
-  const int rhi = int(min<int64_t>(g.nx - 2 - g.gx0, int64_t(1) << 30));
+  int rlo = int(max<int64_t>(1 - g.gx0, -(int64_t(1) << 30)));
+  int rhi = int(min<int64_t>(g.nx - 2 - g.gx0, int64_t(1) << 30));
+  if ((a.flags & tbdetail::kTbAltDirection) && (chunk & 1)) {
+    // Stream this chunk bottom-up: mirror rows r -> M - r about the chunk
+    // (the same row set [rb-K, re+K) is read, [rb, re) written).
+    const int64_t M = rb + re - 1;
+    src += M * pitch;
+    dst += M * pitch;
+    pitch = -pitch;
+    const int lo = rlo, hi = rhi;
+    rlo = int(max<int64_t>(M - hi, -(int64_t(1) << 30)));
+    rhi = int(min<int64_t>(M - lo, int64_t(1) << 30));
+  }
   unsigned m = 0;
   // Which Dirichlet mode this wave needs (all wave-uniform).
   const bool rows_in = gx_lo >= 1 && gx_hi <= g.nx - 2;
@@ -356,7 +373,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     }
     TbStream<K, LAG, MD> st;
     st.rc = int(min<int64_t>(cend - col, 4));
-    st.run(src, dst, g.pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
+    st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
     m = st.m;
   };
   switch (mode) {

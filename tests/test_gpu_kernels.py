@@ -49,7 +49,9 @@ def test_naive_step_vs_torch(gpu):
     torch.testing.assert_close(b.owned(), ref, rtol=1e-6, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4, 7])
+# 0/3 packed ring-3 (+ramp), 4/7 scalar; +16 XCD-grouped blocks, +32 odd
+# chunks streamed bottom-up (mirrored rows, incl. the plate's top/bottom rows).
+@pytest.mark.parametrize("variant", [0, 3, 4, 7, 23, 39, 55])
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     lx, ly = 203, 517  # odd sizes: partial strips and chunks
@@ -61,11 +63,12 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
+@pytest.mark.parametrize("variant", [7, 55])
 @pytest.mark.parametrize("waves", [64, 4096])
-def test_tb_chunking_invariance(gpu, waves):
+def test_tb_chunking_invariance(gpu, waves, variant):
     lx, ly, k = 300, 1000, 8
     g, a, b = _fields(lx, ly, k, gpu)
-    ops.tb_step(a, b, g, k, waves_target=waves)
+    ops.tb_step(a, b, g, k, waves_target=waves, variant=variant)
     torch.cuda.synchronize()
     ref = _cpu_steps(g, lx, ly, k, k)
     assert torch.equal(b.owned().cpu(), ref)
