@@ -49,6 +49,7 @@ void usage() {
       "  --no-graph --no-overlap disable hipGraph capture / comm overlap\n"
       "  --schedule auto|sync|overlap|pipeline   multi-rank pass schedule [auto=sync]\n"
       "  --halo-passes M         sync schedule: passes per halo exchange [auto]\n"
+      "  --numerics fp32|mpi     update arithmetic (mpi = reference MPI double) [fp32]\n"
       "  --checkpoint PATH --checkpoint-every K   periodic binary checkpoints\n"
       "  --resume PATH           start from a binary checkpoint\n"
       "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
@@ -89,7 +90,12 @@ int main(int argc, char** argv) {
     else if (a == "--cy") P.cy = float(std::atof(need().c_str()));
     else if (a == "--converge") P.converge = true;
     else if (a == "--check-interval") P.check_interval = std::atoi(need().c_str());
-    else if (a == "--eps") P.eps = float(std::atof(need().c_str()));
+    else if (a == "--eps") P.eps = std::atof(need().c_str());
+    else if (a == "--numerics") {
+      std::string n = need();
+      HEAT_CHECK(n == "fp32" || n == "mpi", "--numerics fp32|mpi, got %s", n.c_str());
+      P.numerics = n == "mpi" ? Numerics::Mpi : Numerics::Fp32;
+    }
     else if (a == "--backend") {
       std::string b = need();
       backend_set = true;

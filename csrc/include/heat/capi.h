@@ -23,7 +23,7 @@ typedef struct heat_params {
   int64_t nx, ny;
   float cx, cy;
   int32_t converge, check_interval;
-  float eps;
+  double eps;
   int32_t init;      /* heat::InitMode */
   uint64_t seed;
   int32_t backend;   /* 0 cpu, 1 hip */
@@ -37,6 +37,8 @@ typedef struct heat_params {
   int32_t device;
   int32_t schedule;    /* 0 auto, 1 sync, 2 overlap (exchange-first), 3 pipeline */
   int32_t halo_passes; /* sync schedule: passes per exchange (0 = auto) */
+  int32_t numerics;    /* 0 fp32 (canonical FMA), 1 mpi (reference MPI double arithmetic) */
+  int32_t pad_;
 } heat_params;
 
 /* Transport selection for heat_solver_create. */

@@ -16,6 +16,7 @@ struct Geom {
   int64_t gx0 = 0, gy0 = 0;
   int64_t nx = 0, ny = 0;
   float cx = 0.1f, cy = 0.1f;
+  int numerics = 0;  // heat::Numerics
 };
 
 void set_threads(int n);

@@ -73,4 +73,18 @@ HEAT_HD inline float stencil(float c, float n, float s, float w, float e, float 
   return __builtin_fmaf(cy, ty, __builtin_fmaf(cx, tx, c));
 }
 
+// The reference MPI program's update (mpi/mpi_heat_improved_persistent_stat.c:
+// 168-174): the two neighbour sums are fp32 additions (float + float in C),
+// everything else is double because of the 2.0 literal, evaluated left to
+// right without contraction, and the result is rounded to fp32 once.
+HEAT_HD inline float stencil_mpi(float c, float n, float s, float w, float e, float cx,
+                                 float cy) {
+#pragma clang fp contract(off)
+  const float ns = s + n;
+  const float ew = e + w;
+  const double dc = double(c);
+  const double a = dc + double(cx) * (double(ns) - 2.0 * dc);
+  return float(a + double(cy) * (double(ew) - 2.0 * dc));
+}
+
 }  // namespace heat

@@ -28,6 +28,7 @@ struct StencilGeom {
   int64_t gx0 = 0, gy0 = 0;
   int64_t nx = 0, ny = 0;
   float cx = 0.1f, cy = 0.1f;
+  int numerics = 0;  // heat::Numerics (naive kernel only; TB is always Fp32)
 };
 
 // Depths the temporally blocked kernel is instantiated for.

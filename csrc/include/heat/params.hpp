@@ -45,6 +45,15 @@ enum class DecompKind : int {
   Grid2D = 2,
 };
 
+// Arithmetic of the update.
+enum class Numerics : int {
+  Fp32 = 0,  // canonical fp32 FMA expression, heat::stencil (= the reference CUDA
+             // kernel's expression under nvcc's default contraction); every kernel
+  Mpi = 1,   // the reference MPI program's: fp32 neighbour sums, the rest in
+             // double (its 2.0 literal), one rounding to fp32; heat::stencil_mpi.
+             // CPU backend and the naive GPU kernel only.
+};
+
 // Pass schedule of a multi-rank GPU run (the reference overlaps
 // inner-cell compute with MPI_Isend/Irecv).  Measured on MI355X
 // (profiles/overlap_probe_r1.md): cross-queue event hops cost ~10 us and
@@ -67,7 +76,7 @@ struct Params {
   float cy = 0.1f;  // PARMS_CY / parms.cy
   bool converge = false;   // -DCONVERGE
   int check_interval = 20; // CHECK_INTERVAL / STEP
-  float eps = 1e-3f;       // literal 1e-3 of the reference
+  double eps = 1e-3;       // literal 1e-3 of the reference (a double in mpi/...c:245)
   InitMode init = InitMode::RefWrap;
   uint64_t seed = 0;
   Backend backend = Backend::Cpu;
@@ -82,11 +91,13 @@ struct Params {
   int device = -1;          // HIP device ordinal (-1 = local rank % device count)
   Schedule schedule = Schedule::Auto;
   int halo_passes = 0;      // passes per exchange with Sync (ghost depth m*K); 0 = auto
+  Numerics numerics = Numerics::Fp32;
 };
 
 const char* init_mode_name(InitMode m);
 const char* kernel_name(KernelKind k);
 const char* compat_name(Compat c);
 const char* schedule_name(Schedule s);
+const char* numerics_name(Numerics n);
 
 }  // namespace heat

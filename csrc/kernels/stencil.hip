@@ -66,7 +66,9 @@ __global__ __launch_bounds__(256) void naive_kernel(const float* __restrict__ sr
     const float v = src[i];
     float out = v;
     if (in_interior(g.gx0 + r, g.nx) && in_interior(g.gy0 + c, g.ny))
-      out = stencil(v, src[i - g.pitch], src[i + g.pitch], src[i - 1], src[i + 1], g.cx, g.cy);
+      out = g.numerics == 1
+                ? stencil_mpi(v, src[i - g.pitch], src[i + g.pitch], src[i - 1], src[i + 1], g.cx, g.cy)
+                : stencil(v, src[i - g.pitch], src[i + g.pitch], src[i - 1], src[i + 1], g.cx, g.cy);
     dst[i] = out;
     m = __float_as_uint(fabsf(out - v));
   }

@@ -52,6 +52,14 @@ const char* schedule_name(Schedule s) {
   return "?";
 }
 
+const char* numerics_name(Numerics n) {
+  switch (n) {
+    case Numerics::Fp32: return "fp32";
+    case Numerics::Mpi: return "mpi";
+  }
+  return "?";
+}
+
 Params params_from_c(const heat_params* p) {
   Params P;
   P.nx = p->nx;
@@ -76,6 +84,7 @@ Params params_from_c(const heat_params* p) {
   P.device = p->device;
   P.schedule = Schedule(p->schedule);
   P.halo_passes = p->halo_passes;
+  P.numerics = Numerics(p->numerics);
   return P;
 }
 

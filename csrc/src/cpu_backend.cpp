@@ -45,16 +45,26 @@ float step(const float* src, float* dst, const Geom& g, const Box& box, bool wan
     const float* so = s + g.pitch;
     for (int64_t c = box.c0; c < cl; ++c) d[c] = s[c];
     uint32_t rm = 0;
-    for (int64_t c = cl; c < ch; ++c) {
-      const float v = stencil(s[c], n[c], so[c], s[c - 1], s[c + 1], g.cx, g.cy);
-      d[c] = v;
-      if (want_resid) {
-        float diff = std::fabs(v - s[c]);
-        uint32_t bits;
-        std::memcpy(&bits, &diff, 4);
-        rm = bits > rm ? bits : rm;
+    auto row = [&](auto update) {
+      for (int64_t c = cl; c < ch; ++c) {
+        const float v = update(s[c], n[c], so[c], s[c - 1], s[c + 1], g.cx, g.cy);
+        d[c] = v;
+        if (want_resid) {
+          float diff = std::fabs(v - s[c]);
+          uint32_t bits;
+          std::memcpy(&bits, &diff, 4);
+          rm = bits > rm ? bits : rm;
+        }
       }
-    }
+    };
+    if (g.numerics == 1)
+      row([](float c, float n, float s, float w, float e, float cx, float cy) {
+        return stencil_mpi(c, n, s, w, e, cx, cy);
+      });
+    else
+      row([](float c, float n, float s, float w, float e, float cx, float cy) {
+        return stencil(c, n, s, w, e, cx, cy);
+      });
     for (int64_t c = ch; c < box.c1; ++c) d[c] = s[c];
     mbits = rm > mbits ? rm : mbits;
   }

@@ -43,6 +43,12 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   cart_ = Cart(tr_->world(), P_.decomp, P_.px, P_.py, P_.nx, P_.ny);
   blk_ = make_block(cart_, tr_->rank(), P_.nx, P_.ny);
   if (on_gpu()) {
+    // The TB kernel evaluates the canonical fp32 expression only.
+    if (P_.numerics != Numerics::Fp32) {
+      HEAT_CHECK(P_.kernel != KernelKind::TB, "--numerics %s needs the naive kernel",
+                 numerics_name(P_.numerics));
+      P_.kernel = KernelKind::Naive;
+    }
     if (P_.kernel == KernelKind::Naive) {
       T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
     } else {
@@ -294,6 +300,7 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
   g.ny = P_.ny;
   g.cx = P_.cx;
   g.cy = P_.cy;
+  g.numerics = int(P_.numerics);
   unsigned* r = resid ? d_resid_ : nullptr;
   const int64_t lx = blk_.lx, ly = blk_.ly;
   const auto& nb = blk_.nbr;
@@ -347,6 +354,7 @@ void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
   g.ny = P_.ny;
   g.cx = P_.cx;
   g.cy = P_.cy;
+  g.numerics = int(P_.numerics);
   const auto& nb = blk_.nbr;
   for (int j = 0; j < k; ++j) {
     const int64_t e = k - 1 - j;
@@ -489,7 +497,10 @@ bool Solver::is_check_point(int64_t completed) const {
 }
 
 bool Solver::converged_value(float r) const {
-  return P_.compat == Compat::Mpi ? r <= P_.eps : r < P_.eps;
+  // mpi/...c:245 compares the fp32 |delta| against the double 1e-3;
+  // cuda/cuda_heat.cu:67 compares in fp32 against 1e-3f.
+  if (P_.compat == Compat::Mpi) return double(r) <= P_.eps;
+  return r < float(P_.eps);
 }
 
 RunStats Solver::run(int64_t steps) {

@@ -42,7 +42,7 @@ class HeatParams(Structure):
         ("nx", c_int64), ("ny", c_int64),
         ("cx", c_float), ("cy", c_float),
         ("converge", c_int32), ("check_interval", c_int32),
-        ("eps", c_float),
+        ("eps", c_double),
         ("init", c_int32),
         ("seed", c_uint64),
         ("backend", c_int32), ("kernel", c_int32), ("tb_depth", c_int32), ("threads", c_int32),
@@ -50,6 +50,7 @@ class HeatParams(Structure):
         ("use_graph", c_int32), ("overlap", c_int32),
         ("compat", c_int32), ("device", c_int32),
         ("schedule", c_int32), ("halo_passes", c_int32),
+        ("numerics", c_int32), ("pad_", c_int32),
     ]
 
 

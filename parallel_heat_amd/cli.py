@@ -52,6 +52,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--no-overlap", action="store_true")
     a("--schedule", choices=["auto", "sync", "overlap", "pipeline"], default="auto")
     a("--halo-passes", type=int, default=0)
+    a("--numerics", choices=["fp32", "mpi"], default="fp32")
     a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
@@ -70,7 +71,7 @@ def main(argv=None) -> int:
                      tb_depth=args.tb_depth, threads=args.threads, decomp=args.decomp,
                      px=args.px, py=args.py, use_graph=not args.no_graph,
                      overlap=not args.no_overlap, compat=compat, schedule=args.schedule,
-                     halo_passes=args.halo_passes)
+                     halo_passes=args.halo_passes, numerics=args.numerics)
     info = pcomm.init_distributed("nccl" if backend == "hip" else "gloo")
     root = info.is_root
     out = sys.stdout

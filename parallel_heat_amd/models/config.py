@@ -18,6 +18,7 @@ KERNELS = {"auto": 0, "naive": 1, "tb": 2}
 DECOMPS = {"auto": 0, "rows": 1, "1d": 1, "2d": 2}
 COMPATS = {"none": 0, "mpi": 1, "cuda": 2}
 SCHEDULES = {"auto": 0, "sync": 1, "overlap": 2, "pipeline": 3}
+NUMERICS = {"fp32": 0, "mpi": 1}
 
 
 @dataclass
@@ -45,6 +46,7 @@ class HeatConfig:
     device: int = -1
     schedule: str = "auto"        # multi-rank pass schedule: auto(=sync) | sync | overlap | pipeline
     halo_passes: int = 0          # sync: passes per halo exchange (ghost depth m*K); 0 = auto
+    numerics: str = "fp32"        # fp32 (canonical FMA) | mpi (reference MPI double arithmetic)
 
     def replace(self, **kw) -> "HeatConfig":
         return dataclasses.replace(self, **kw)
@@ -54,7 +56,7 @@ class HeatConfig:
             raise ValueError(f"grid {self.nx}x{self.ny}")
         for name, table in (("init", INIT_MODES), ("backend", BACKENDS), ("kernel", KERNELS),
                             ("decomp", DECOMPS), ("compat", COMPATS),
-                            ("schedule", SCHEDULES)):
+                            ("schedule", SCHEDULES), ("numerics", NUMERICS)):
             if getattr(self, name) not in table:
                 raise ValueError(f"{name}={getattr(self, name)!r}; expected one of {sorted(table)}")
         if self.check_interval < 1:
@@ -88,4 +90,5 @@ class HeatConfig:
         p.device = int(self.device if device is None else device)
         p.schedule = SCHEDULES[self.schedule]
         p.halo_passes = int(self.halo_passes)
+        p.numerics = NUMERICS[self.numerics]
         return p

@@ -73,6 +73,26 @@ def step_np(u: np.ndarray, cx: float = 0.1, cy: float = 0.1) -> np.ndarray:
     return out
 
 
+def step_np_mpi(u: np.ndarray, cx: float = 0.1, cy: float = 0.1) -> np.ndarray:
+    """One step with the reference MPI program's arithmetic
+    (mpi/mpi_heat_improved_persistent_stat.c:168-174): the two neighbour sums
+    in float32 (float + float in C), the rest in float64 because of the 2.0
+    literal, evaluated left to right, rounded to float32 once.  NumPy float64
+    ops are IEEE and never fused, so this is the exact oracle of
+    `numerics="mpi"`."""
+    u = np.asarray(u, np.float32)
+    out = u.copy()
+    if u.shape[0] < 3 or u.shape[1] < 3:
+        return out
+    c = u[1:-1, 1:-1].astype(np.float64)
+    ns = (u[2:, 1:-1] + u[:-2, 1:-1]).astype(np.float64)   # float32 add, then widen
+    ew = (u[1:-1, 2:] + u[1:-1, :-2]).astype(np.float64)
+    fcx, fcy = float(np.float32(cx)), float(np.float32(cy))  # parms are float
+    a = c + fcx * (ns - 2.0 * c)
+    out[1:-1, 1:-1] = (a + fcy * (ew - 2.0 * c)).astype(np.float32)
+    return out
+
+
 def step_torch(u: torch.Tensor, cx: float = 0.1, cy: float = 0.1) -> torch.Tensor:
     """The same step as plain PyTorch fp32 ops (any device)."""
     out = u.clone()
@@ -95,16 +115,18 @@ def check_points(total: int, interval: int, compat: str = "none"):
 def run_np(nx: int, ny: int, steps: int, cx: float = 0.1, cy: float = 0.1,
            converge: bool = False, check_interval: int = 20, eps: float = 1e-3,
            compat: str = "none", init: str = "ref-wrap", seed: int = 0,
-           u0: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int, int]:
+           u0: Optional[np.ndarray] = None,
+           numerics: str = "fp32") -> Tuple[np.ndarray, int, int]:
     """Run the model; returns (grid, steps_done, converged_at or -1)."""
+    step = step_np_mpi if numerics == "mpi" else step_np
     u = init_grid(nx, ny, init, seed) if u0 is None else np.array(u0, np.float32)
     total = steps + 1 if compat == "mpi" else steps
     checks = set(check_points(total, check_interval, compat)) if converge else set()
     for k in range(1, total + 1):
-        v = step_np(u, cx, cy)
+        v = step(u, cx, cy)
         if k in checks:
             r = float(np.max(np.abs(v - u))) if v.size else 0.0
-            ok = r <= eps if compat == "mpi" else r < eps
+            ok = r <= eps if compat == "mpi" else r < np.float32(eps)
             if ok:
                 return v, k, k
         u = v

@@ -139,3 +139,36 @@ def test_scatter_single_rank():
     with HeatSolver(cfg.replace(init="random", seed=9)) as s:
         s.run(10)
         assert np.array_equal(s.gather(), a)
+
+
+@pytest.mark.parametrize("nx,ny,steps,init", [(20, 20, 101, "ref-wrap"), (480, 64, 12, "ref-wrap"),
+                                              (37, 53, 60, "random")])
+def test_mpi_numerics_bitwise_vs_numpy_emulation(nx, ny, steps, init):
+    # numerics="mpi" reproduces the reference MPI program's arithmetic
+    # (fp32 neighbour sums, double combine, one rounding) bit for bit.
+    cfg = HeatConfig(nx=nx, ny=ny, steps=steps, init=init, seed=3, backend="cpu",
+                     numerics="mpi", threads=2)
+    g, _ = run(cfg)
+    ref, _, _ = R.run_np(nx, ny, steps, init=init, seed=3, numerics="mpi")
+    assert np.array_equal(g, ref)
+    # and it is a genuinely different rounding from the canonical fp32 FMA form
+    g32, _ = run(cfg.replace(numerics="fp32"))
+    assert np.abs(g32 - ref).max() <= 1e-5 * max(1.0, float(np.abs(ref).max()))
+
+
+def test_mpi_numerics_convergence_vs_numpy_emulation():
+    kw = dict(nx=20, ny=20, steps=10000, converge=True, check_interval=20, eps=1e-3)
+    g, r = run(HeatConfig(**kw, backend="cpu", numerics="mpi", compat="mpi"))
+    ref, done, conv_at = R.run_np(**kw, compat="mpi", numerics="mpi")
+    assert r.converged and r.converged_at == conv_at
+    assert np.array_equal(g, ref)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_mpi_numerics_decomposition_invariance(tmp_path, world):
+    from .dist_worker import run_world
+    kw = dict(nx=40, ny=36, steps=0, init="random", seed=5, backend="cpu", numerics="mpi",
+              tb_depth=2, halo_passes=2)
+    res = run_world(world, kw, 25, tmp_path)
+    ref, _, _ = R.run_np(40, 36, 25, init="random", seed=5, numerics="mpi")
+    assert np.array_equal(res["grid"], ref)

@@ -104,3 +104,16 @@ def test_gpu_scatter(gpu):
     with HeatSolver(cfg.replace(init="random", seed=5)) as s:
         s.run(17)
         assert np.array_equal(s.gather(), a)
+
+
+def test_gpu_mpi_numerics(gpu):
+    # numerics="mpi" runs on the naive kernel (auto-selected) and reproduces
+    # the reference MPI program's double arithmetic bit for bit.
+    from parallel_heat_amd.models import reference as R
+    cfg = HeatConfig(nx=96, ny=130, steps=33, init="random", seed=4, backend="hip",
+                     numerics="mpi")
+    g, _ = _run(cfg)
+    ref, _, _ = R.run_np(96, 130, 33, init="random", seed=4, numerics="mpi")
+    assert np.array_equal(g, ref)
+    with pytest.raises(Exception, match="naive"):
+        HeatSolver(cfg.replace(kernel="tb"))
