@@ -43,7 +43,7 @@ typedef struct heat_params {
 
 /* Transport selection for heat_solver_create. */
 typedef struct heat_comm {
-  int32_t kind;          /* 0 local, 1 rccl, 2 tcp, 3 callback */
+  int32_t kind;          /* 0 local, 1 rccl, 2 tcp, 3 callback, 4 loopback (ctx = hub) */
   int32_t rank, world;
   int32_t device;        /* rccl: HIP device */
   uint8_t unique_id[128];/* rccl: ncclUniqueId from heat_rccl_unique_id on rank 0 */
@@ -94,6 +94,9 @@ int heat_device_count(int* n);
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out);
 int heat_solver_destroy(heat_solver* s);
 int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
+/* Loopback transport: ranks are threads of this process sharing one hub. */
+int heat_loopback_hub_create(int world, void** out);
+int heat_loopback_hub_destroy(void* hub);
 int heat_solver_reset(heat_solver* s);
 int heat_solver_info(heat_solver* s, heat_block_info* out);
 int heat_solver_step(heat_solver* s, int64_t* out);

@@ -18,6 +18,9 @@
 //   CallbackTransport  host memory; the wire is supplied by the embedding
 //                      program (the Python package routes it through
 //                      torch.distributed, e.g. gloo on CPU).
+//   LoopbackTransport  several ranks as threads of one process, device
+//                      memory, stream-ordered D2D/peer copies: tests the
+//                      RCCL-shaped path on one GPU; single-process multi-GPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -75,6 +78,13 @@ void rccl_unique_id(void* out128);
 // (full mesh, one socket per peer pair).
 std::unique_ptr<Transport> make_tcp_transport(int rank, int world, const std::string& addr,
                                               int port);
+
+// Loopback: ranks are host threads of one process sharing a hub; device
+// buffers, stream-ordered device-to-device (or peer) copies.
+struct LoopbackHub;
+LoopbackHub* loopback_hub_create(int world);
+void loopback_hub_destroy(LoopbackHub* hub);
+std::unique_ptr<Transport> make_loopback_transport(LoopbackHub* hub, int rank, int device);
 
 // Callback transport (C ABI so foreign runtimes can implement it).
 extern "C" {

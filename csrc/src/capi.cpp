@@ -146,6 +146,14 @@ int heat_device_count(int* n) {
   });
 }
 
+int heat_loopback_hub_create(int world, void** out) {
+  return guard([&] { *out = heat::loopback_hub_create(world); });
+}
+
+int heat_loopback_hub_destroy(void* hub) {
+  return guard([&] { heat::loopback_hub_destroy(static_cast<heat::LoopbackHub*>(hub)); });
+}
+
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out) {
   return guard([&] {
     heat::Params P = heat::params_from_c(p);
@@ -172,6 +180,11 @@ int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** o
         tr = heat::make_callback_transport(cb);
         break;
       }
+      case 4:
+        tr = heat::make_loopback_transport(static_cast<heat::LoopbackHub*>(c->ctx), c->rank,
+                                           c->device);
+        if (P.device < 0) P.device = c->device;
+        break;
       default:
         HEAT_CHECK(false, "unknown transport kind %d", c->kind);
     }

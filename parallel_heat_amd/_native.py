@@ -110,6 +110,8 @@ _SIGS = {
     "heat_solver_create": (c_int, [POINTER(HeatParams), POINTER(HeatComm), POINTER(c_void_p)]),
     "heat_solver_destroy": (c_int, [c_void_p]),
     "heat_solver_run": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
+    "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "heat_loopback_hub_destroy": (c_int, [c_void_p]),
     "heat_solver_reset": (c_int, [c_void_p]),
     "heat_solver_info": (c_int, [c_void_p, POINTER(HeatBlockInfo)]),
     "heat_solver_step": (c_int, [c_void_p, POINTER(c_int64)]),

@@ -79,7 +79,8 @@ class HeatSolver:
     """One rank of a heat-diffusion run on the native MI355X engine."""
 
     def __init__(self, config: HeatConfig, transport: str = "auto",
-                 dist_info: Optional[pcomm.DistInfo] = None, device: Optional[int] = None):
+                 dist_info: Optional[pcomm.DistInfo] = None, device: Optional[int] = None,
+                 hub: Optional[pcomm.LoopbackHub] = None):
         self.config = config
         config.validate()
         if config.backend == "hip":
@@ -102,7 +103,8 @@ class HeatSolver:
                 device = -1
         self.device = device
         self.transport = transport
-        self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0))
+        self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0),
+                                                 hub=hub)
         params = config.to_native(device=device)
         h = ctypes.c_void_p()
         _native.call("heat_solver_create", ctypes.byref(params), ctypes.byref(self._comm),

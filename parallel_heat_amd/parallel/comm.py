@@ -150,12 +150,41 @@ def broadcast_bytes(data: Optional[bytes], src: int = 0) -> bytes:
     return obj[0]
 
 
+class LoopbackHub:
+    """Native hub of the loopback transport: `world` ranks that are threads of
+    this process (see csrc/src/transport_loopback.cpp)."""
+
+    def __init__(self, world: int):
+        h = ctypes.c_void_p()
+        _native.call("heat_loopback_hub_create", int(world), ctypes.byref(h))
+        self.world = world
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            _native.call("heat_loopback_hub_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = None,
-              port: Optional[int] = None):
+              port: Optional[int] = None, hub: Optional[LoopbackHub] = None):
     """Build a native HeatComm (and the Python object that must outlive it)."""
     comm = _native.HeatComm()
     keep = None
-    if info.world == 1 or kind == "local":
+    if kind == "loopback":
+        if hub is None:
+            raise ValueError("the loopback transport needs a LoopbackHub")
+        comm.kind = 4
+        comm.rank, comm.world, comm.device = info.rank, hub.world, device
+        comm.ctx = hub.handle
+        keep = hub
+    elif info.world == 1 or kind == "local":
         comm.kind = 0
         comm.rank, comm.world = 0, 1
     elif kind == "rccl":
