@@ -49,6 +49,10 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--schedule", default="auto", help="multi-rank pass schedule")
+    ap.add_argument("--halo-passes", type=int, default=0)
+    ap.add_argument("--phase-timing", action="store_true",
+                    help="diagnostic: eager run with per-phase device times (not the headline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,7 +76,9 @@ def main() -> int:
                      backend="hip", kernel=args.kernel, tb_depth=args.tb_depth,
                      decomp=args.decomp, converge=args.converge,
                      check_interval=args.check_interval, use_graph=not args.no_graph,
-                     overlap=not args.no_overlap, device=local_rank % torch.cuda.device_count())
+                     overlap=not args.no_overlap, device=local_rank % torch.cuda.device_count(),
+                     schedule=args.schedule, halo_passes=args.halo_passes,
+                     phase_timing=args.phase_timing)
     solver = HeatSolver(cfg, dist_info=DistInfo(rank, world, local_rank))
 
     def barrier():
@@ -85,9 +91,11 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done = 0
+    phases = [0.0, 0.0, 0.0]
     for _ in range(args.steps):
         r = solver.run(args.iters_per_step)
         done += r.steps_done
+        phases = [phases[0] + r.t_exchange, phases[1] + r.t_compute, phases[2] + r.t_reduce]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -128,6 +136,10 @@ def main() -> int:
         }
         if args.verbose:
             line["native"] = _native.loaded_path()
+        if args.phase_timing:
+            line["phase_seconds_rank0"] = {"exchange": round(phases[0], 6),
+                                           "compute": round(phases[1], 6),
+                                           "reduce": round(phases[2], 6)}
         print(json.dumps(line), flush=True)
     solver.close()
     if world > 1:

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "heat/capi.h"
@@ -54,6 +55,8 @@ void usage() {
       "  --resume PATH           start from a binary checkpoint\n"
       "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
       "  --port P                rendezvous port (default MASTER_PORT+1 or 29600)\n"
+      "  --gpus N                one process, N GPU ranks as threads (loopback/peer copies)\n"
+      "  --phase-timing          per-phase times (exchange/compute/reduce) in --json; eager\n"
       "  --json                  print a JSON metrics line\n");
 }
 
@@ -62,17 +65,155 @@ int env_i(const char* n, int d) {
   return v && *v ? std::atoi(v) : d;
 }
 
+// Command-line options that shape one rank's run (beyond Params).
+struct Options {
+  int64_t steps = 10000;
+  std::string out, out_format = "dat", naming = "plain";
+  std::string checkpoint, resume;
+  int64_t ckpt_every = 0;
+  bool json = false, dump_initial = false;
+};
+
+// One rank's whole run: banners, solver, output, reference-style lines.
+void run_rank(const Options& o, const Params& P, std::unique_ptr<Transport> tr) {
+  const int rank = tr->rank(), world = tr->world();
+  const bool root = rank == 0;
+
+  // Reference-style banners (mpi/...c:90-96).
+  if (root && o.naming == "mpi") {
+    std::printf("Starting mpi_heat2D with %d worker tasks.\n", world);
+    if (!P.converge)
+      std::printf("Grid size: X= %lld  Y= %lld  Time steps= %lld\n", (long long)P.nx,
+                  (long long)P.ny, (long long)o.steps);
+    else
+      std::printf("Grid size: X= %lld  Y= %lld  Time steps= - \n", (long long)P.nx,
+                  (long long)P.ny);
+    std::fflush(stdout);
+  }
+
+  Solver S(P, std::move(tr));
+  if (!o.resume.empty()) S.read_bin(o.resume);
+
+  const bool small = P.nx * P.ny <= (int64_t(1) << 24);
+  std::string init_path, final_path;
+  if (o.naming == "mpi") {
+    init_path = "initial_im.dat";
+    final_path = "final_im.dat";
+  } else if (o.naming == "cuda") {
+    // out_cuda_<TPB>_<NB>_<STEPS>.dat with the reference's geometry
+    // (THREADS_PER_ROW 32, cuda/cuda_heat.cu:17-21, :245-250).
+    const int64_t T = 32;
+    const int64_t rb = (P.nx - 2) / T + ((P.nx - 2) % T ? 1 : 0);
+    const int64_t cb = (P.ny - 2) / T + ((P.ny - 2) % T ? 1 : 0);
+    final_path = strprintf("out_cuda_%lld_%lld_%lld.dat", (long long)(T * T),
+                           (long long)(rb * cb), (long long)o.steps);
+  } else {
+    final_path = small ? "final.dat" : "none";
+    init_path = "initial.dat";
+  }
+  if (!o.out.empty()) final_path = o.out;
+
+  auto emit = [&](const std::string& path) {
+    if (path == "none" || path.empty()) return;
+    if (o.out_format == "bin") {
+      S.write_bin(path);
+    } else if (o.out_format == "checksum") {
+      Checksum c = S.checksum();
+      if (root) {
+        FILE* f = std::fopen(path.c_str(), "w");
+        HEAT_CHECK(f, "cannot open %s", path.c_str());
+        std::fprintf(f,
+                     "{\"nx\": %lld, \"ny\": %lld, \"step\": %lld, \"hash\": \"%016llx\", "
+                     "\"sum\": %.17g, \"min\": %.9g, \"max\": %.9g, \"count\": %lld}\n",
+                     (long long)P.nx, (long long)P.ny, (long long)S.step(),
+                     (unsigned long long)c.hash, c.sum, c.min, c.max, (long long)c.count);
+        std::fclose(f);
+      }
+    } else {
+      auto g = S.gather_root();
+      if (root) write_dat(path, P.nx, P.ny, g.data());
+    }
+  };
+  if (o.dump_initial || o.naming == "mpi") emit(init_path);
+
+  const int64_t total = S.configured_steps(o.steps);
+  int64_t todo = total - S.step();
+  RunStats acc;
+  while (todo > 0) {
+    const int64_t chunk = o.ckpt_every > 0 ? std::min(o.ckpt_every, todo) : todo;
+    RunStats r = S.run(chunk);
+    acc.steps_done += r.steps_done;
+    acc.seconds += r.seconds;
+    acc.passes += r.passes;
+    acc.exchanges += r.exchanges;
+    acc.checks += r.checks;
+    acc.t_exchange += r.t_exchange;
+    acc.t_compute += r.t_compute;
+    acc.t_reduce += r.t_reduce;
+    acc.last_resid = r.last_resid;
+    todo -= r.steps_done;
+    if (!o.checkpoint.empty() && o.ckpt_every > 0) S.write_bin(o.checkpoint);
+    if (r.converged) {
+      acc.converged = true;
+      acc.converged_at = r.converged_at;
+      break;
+    }
+  }
+  emit(final_path);
+
+  if (root) {
+    if (P.converge) {
+      if (o.naming == "mpi") {
+        if (acc.converged) std::printf("Converged after %lld steps\n", (long long)(acc.converged_at - 1));
+        else std::printf("Didn't converged\n");
+      } else if (o.naming == "cuda") {
+        if (acc.converged) std::printf("Converged at %lld steps\n", (long long)(acc.converged_at - 1));
+        else std::printf("Did not converge\n");
+      } else {
+        if (acc.converged) std::printf("Converged after %lld steps\n", (long long)acc.converged_at);
+        else std::printf("Did not converge after %lld steps\n", (long long)S.step());
+      }
+    }
+    const double secs = acc.seconds;
+    if (o.naming == "cuda") {
+      const double ms = secs * 1e3;
+      std::printf("Elapsed time: %.3f %ssecs\n", ms / 1000 > 1.0 ? ms / 1000 : ms,
+                  ms / 1000 > 1.0 ? "" : "m");
+    } else {
+      std::printf("Elapsed time %f secs\n", secs);
+    }
+    const double cells = double(P.nx) * double(P.ny) * double(acc.steps_done);
+    if (o.json) {
+      const auto& c = S.cart();
+      std::printf(
+          "{\"nx\": %lld, \"ny\": %lld, \"steps\": %lld, \"steps_done\": %lld, \"ranks\": %d, "
+          "\"backend\": \"%s\", \"decomp\": \"%dx%d\", \"tb_depth\": %d, \"seconds\": %.6f, "
+          "\"mcells_per_s\": %.3f, \"s_per_1000_iters\": %.6f, \"converged\": %s, "
+          "\"converged_at\": %lld, \"last_resid\": %.6g, \"passes\": %lld, \"exchanges\": %lld, "
+          "\"transport\": \"%s\", \"schedule\": \"%s\", \"halo\": %d, \"t_exchange\": %.6f, "
+          "\"t_compute\": %.6f, \"t_reduce\": %.6f}\n",
+          (long long)P.nx, (long long)P.ny, (long long)total, (long long)acc.steps_done, world,
+          P.backend == Backend::Hip ? "hip" : "cpu", c.px, c.py, S.tb_depth(), secs,
+          secs > 0 ? cells / secs / 1e6 : 0.0,
+          acc.steps_done > 0 ? secs * 1000.0 / double(acc.steps_done) : 0.0,
+          acc.converged ? "true" : "false", (long long)acc.converged_at, double(acc.last_resid),
+          (long long)acc.passes, (long long)acc.exchanges, S.transport().name(),
+          schedule_name(S.schedule()), S.halo(), acc.t_exchange, acc.t_compute, acc.t_reduce);
+    }
+    std::fflush(stdout);
+  }
+  S.barrier();
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Params P;
-  int64_t steps = 10000;
-  std::string out, out_format = "dat", naming = "plain", transport = "auto";
-  std::string checkpoint, resume;
-  int64_t ckpt_every = 0;
-  bool json = false, dump_initial = false, backend_set = false;
+  Options o;
+  std::string transport = "auto";
+  int gpus = 0;
+  bool backend_set = false;
   int port = 0;
-  std::map<std::string, std::string> kv;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto need = [&]() -> std::string {
@@ -85,7 +226,7 @@ int main(int argc, char** argv) {
     if (a == "-h" || a == "--help") { usage(); return 0; }
     else if (a == "--nx") P.nx = std::atoll(need().c_str());
     else if (a == "--ny") P.ny = std::atoll(need().c_str());
-    else if (a == "--steps") steps = std::atoll(need().c_str());
+    else if (a == "--steps") o.steps = std::atoll(need().c_str());
     else if (a == "--cx") P.cx = float(std::atof(need().c_str()));
     else if (a == "--cy") P.cy = float(std::atof(need().c_str()));
     else if (a == "--converge") P.converge = true;
@@ -120,10 +261,10 @@ int main(int argc, char** argv) {
                : m == "zero"                ? InitMode::Zero
                                             : InitMode::RefWrap;
     } else if (a == "--seed") P.seed = std::strtoull(need().c_str(), nullptr, 10);
-    else if (a == "--out") out = need();
-    else if (a == "--out-format") out_format = need();
-    else if (a == "--naming") naming = need();
-    else if (a == "--dump-initial") dump_initial = true;
+    else if (a == "--out") o.out = need();
+    else if (a == "--out-format") o.out_format = need();
+    else if (a == "--naming") o.naming = need();
+    else if (a == "--dump-initial") o.dump_initial = true;
     else if (a == "--compat") {
       std::string c = need();
       P.compat = c == "mpi" ? Compat::Mpi : c == "cuda" ? Compat::Cuda : Compat::None;
@@ -138,16 +279,18 @@ int main(int argc, char** argv) {
                    : s == "pipeline" ? Schedule::Pipeline
                                      : Schedule::Auto;
     } else if (a == "--halo-passes") P.halo_passes = std::atoi(need().c_str());
-    else if (a == "--checkpoint") checkpoint = need();
-    else if (a == "--checkpoint-every") ckpt_every = std::atoll(need().c_str());
-    else if (a == "--resume") resume = need();
+    else if (a == "--checkpoint") o.checkpoint = need();
+    else if (a == "--checkpoint-every") o.ckpt_every = std::atoll(need().c_str());
+    else if (a == "--resume") o.resume = need();
     else if (a == "--transport") transport = need();
     else if (a == "--port") port = std::atoi(need().c_str());
-    else if (a == "--json") json = true;
+    else if (a == "--json") o.json = true;
+    else if (a == "--gpus") gpus = std::atoi(need().c_str());
+    else if (a == "--phase-timing") P.phase_timing = true;
     else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
   }
-  if (naming == "mpi" && P.compat == Compat::None) P.compat = Compat::Mpi;
-  if (naming == "cuda" && P.compat == Compat::None) P.compat = Compat::Cuda;
+  if (o.naming == "mpi" && P.compat == Compat::None) P.compat = Compat::Mpi;
+  if (o.naming == "cuda" && P.compat == Compat::None) P.compat = Compat::Cuda;
 
   const int world = env_i("WORLD_SIZE", 1), rank = env_i("RANK", 0);
   const int local_rank = env_i("LOCAL_RANK", rank);
@@ -163,6 +306,37 @@ int main(int argc, char** argv) {
     return 1;
   }
   if (P.backend == Backend::Hip) P.device = local_rank % ndev;
+
+  if (gpus > 1 && world == 1) {
+    // One process, `gpus` ranks as threads over the loopback transport
+    // (peer copies between devices; ranks share devices round-robin when
+    // fewer GPUs are visible).
+    if (P.backend != Backend::Hip) {
+      std::fprintf(stderr, "heat: --gpus needs the hip backend\n");
+      return 2;
+    }
+    LoopbackHub* hub = loopback_hub_create(gpus);
+    std::vector<std::thread> threads;
+    std::vector<std::string> errors(gpus);
+    for (int r = 0; r < gpus; ++r)
+      threads.emplace_back([&, r] {
+        try {
+          Params Pr = P;
+          Pr.device = r % ndev;
+          run_rank(o, Pr, make_loopback_transport(hub, r, Pr.device));
+        } catch (const std::exception& e) {
+          errors[r] = e.what();
+        }
+      });
+    for (auto& t : threads) t.join();
+    loopback_hub_destroy(hub);
+    for (int r = 0; r < gpus; ++r)
+      if (!errors[r].empty()) {
+        std::fprintf(stderr, "heat: rank %d error: %s\n", r, errors[r].c_str());
+        return 1;
+      }
+    return 0;
+  }
 
   try {
     std::unique_ptr<Transport> tr;
@@ -188,129 +362,7 @@ int main(int argc, char** argv) {
     } else {
       tr = make_tcp_transport(rank, world, addr, port);
     }
-    const bool root = rank == 0;
-
-    // Reference-style banners (mpi/...c:90-96).
-    if (root && naming == "mpi") {
-      std::printf("Starting mpi_heat2D with %d worker tasks.\n", world);
-      if (!P.converge)
-        std::printf("Grid size: X= %lld  Y= %lld  Time steps= %lld\n", (long long)P.nx,
-                    (long long)P.ny, (long long)steps);
-      else
-        std::printf("Grid size: X= %lld  Y= %lld  Time steps= - \n", (long long)P.nx,
-                    (long long)P.ny);
-      std::fflush(stdout);
-    }
-
-    const double t_init0 = 0;
-    (void)t_init0;
-    Solver S(P, std::move(tr));
-    if (!resume.empty()) S.read_bin(resume);
-
-    const bool small = P.nx * P.ny <= (int64_t(1) << 24);
-    std::string init_path, final_path;
-    if (naming == "mpi") {
-      init_path = "initial_im.dat";
-      final_path = "final_im.dat";
-    } else if (naming == "cuda") {
-      // out_cuda_<TPB>_<NB>_<STEPS>.dat with the reference's geometry
-      // (THREADS_PER_ROW 32, cuda/cuda_heat.cu:17-21, :245-250).
-      const int64_t T = 32;
-      const int64_t rb = (P.nx - 2) / T + ((P.nx - 2) % T ? 1 : 0);
-      const int64_t cb = (P.ny - 2) / T + ((P.ny - 2) % T ? 1 : 0);
-      final_path = strprintf("out_cuda_%lld_%lld_%lld.dat", (long long)(T * T),
-                             (long long)(rb * cb), (long long)steps);
-    } else {
-      final_path = small ? "final.dat" : "none";
-      init_path = "initial.dat";
-    }
-    if (!out.empty()) final_path = out;
-
-    auto emit = [&](const std::string& path) {
-      if (path == "none" || path.empty()) return;
-      if (out_format == "bin") {
-        S.write_bin(path);
-      } else if (out_format == "checksum") {
-        Checksum c = S.checksum();
-        if (root) {
-          FILE* f = std::fopen(path.c_str(), "w");
-          HEAT_CHECK(f, "cannot open %s", path.c_str());
-          std::fprintf(f,
-                       "{\"nx\": %lld, \"ny\": %lld, \"step\": %lld, \"hash\": \"%016llx\", "
-                       "\"sum\": %.17g, \"min\": %.9g, \"max\": %.9g, \"count\": %lld}\n",
-                       (long long)P.nx, (long long)P.ny, (long long)S.step(),
-                       (unsigned long long)c.hash, c.sum, c.min, c.max, (long long)c.count);
-          std::fclose(f);
-        }
-      } else {
-        auto g = S.gather_root();
-        if (root) write_dat(path, P.nx, P.ny, g.data());
-      }
-    };
-    if (dump_initial || naming == "mpi") emit(init_path);
-
-    const int64_t total = S.configured_steps(steps);
-    int64_t todo = total - S.step();
-    RunStats acc;
-    while (todo > 0) {
-      const int64_t chunk = ckpt_every > 0 ? std::min(ckpt_every, todo) : todo;
-      RunStats r = S.run(chunk);
-      acc.steps_done += r.steps_done;
-      acc.seconds += r.seconds;
-      acc.passes += r.passes;
-      acc.exchanges += r.exchanges;
-      acc.checks += r.checks;
-      acc.last_resid = r.last_resid;
-      todo -= r.steps_done;
-      if (!checkpoint.empty() && ckpt_every > 0) S.write_bin(checkpoint);
-      if (r.converged) {
-        acc.converged = true;
-        acc.converged_at = r.converged_at;
-        break;
-      }
-    }
-    emit(final_path);
-
-    if (root) {
-      if (P.converge) {
-        if (naming == "mpi") {
-          if (acc.converged) std::printf("Converged after %lld steps\n", (long long)(acc.converged_at - 1));
-          else std::printf("Didn't converged\n");
-        } else if (naming == "cuda") {
-          if (acc.converged) std::printf("Converged at %lld steps\n", (long long)(acc.converged_at - 1));
-          else std::printf("Did not converge\n");
-        } else {
-          if (acc.converged) std::printf("Converged after %lld steps\n", (long long)acc.converged_at);
-          else std::printf("Did not converge after %lld steps\n", (long long)S.step());
-        }
-      }
-      const double secs = acc.seconds;
-      if (naming == "cuda") {
-        const double ms = secs * 1e3;
-        std::printf("Elapsed time: %.3f %ssecs\n", ms / 1000 > 1.0 ? ms / 1000 : ms,
-                    ms / 1000 > 1.0 ? "" : "m");
-      } else {
-        std::printf("Elapsed time %f secs\n", secs);
-      }
-      const double cells = double(P.nx) * double(P.ny) * double(acc.steps_done);
-      if (json) {
-        const auto& c = S.cart();
-        std::printf(
-            "{\"nx\": %lld, \"ny\": %lld, \"steps\": %lld, \"steps_done\": %lld, \"ranks\": %d, "
-            "\"backend\": \"%s\", \"decomp\": \"%dx%d\", \"tb_depth\": %d, \"seconds\": %.6f, "
-            "\"mcells_per_s\": %.3f, \"s_per_1000_iters\": %.6f, \"converged\": %s, "
-            "\"converged_at\": %lld, \"last_resid\": %.6g, \"passes\": %lld, \"exchanges\": %lld, "
-            "\"transport\": \"%s\"}\n",
-            (long long)P.nx, (long long)P.ny, (long long)total, (long long)acc.steps_done, world,
-            P.backend == Backend::Hip ? "hip" : "cpu", c.px, c.py, S.tb_depth(), secs,
-            secs > 0 ? cells / secs / 1e6 : 0.0,
-            acc.steps_done > 0 ? secs * 1000.0 / double(acc.steps_done) : 0.0,
-            acc.converged ? "true" : "false", (long long)acc.converged_at, double(acc.last_resid),
-            (long long)acc.passes, (long long)acc.exchanges, S.transport().name());
-      }
-      std::fflush(stdout);
-    }
-    S.barrier();
+    run_rank(o, P, std::move(tr));
   } catch (const std::exception& e) {
     std::fprintf(stderr, "heat: error: %s\n", e.what());
     return 1;

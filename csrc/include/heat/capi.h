@@ -38,7 +38,7 @@ typedef struct heat_params {
   int32_t schedule;    /* 0 auto, 1 sync, 2 overlap (exchange-first), 3 pipeline */
   int32_t halo_passes; /* sync schedule: passes per exchange (0 = auto) */
   int32_t numerics;    /* 0 fp32 (canonical FMA), 1 mpi (reference MPI double arithmetic) */
-  int32_t pad_;
+  int32_t phase_timing;/* 1: per-phase times in heat_run_stats (disables graphs) */
 } heat_params;
 
 /* Transport selection for heat_solver_create. */
@@ -63,6 +63,7 @@ typedef struct heat_run_stats {
   float last_resid;
   double seconds;
   int64_t passes, exchanges, checks;
+  double t_exchange, t_compute, t_reduce; /* seconds per phase (phase_timing) */
 } heat_run_stats;
 
 typedef struct heat_block_info {

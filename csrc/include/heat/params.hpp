@@ -92,6 +92,7 @@ struct Params {
   Schedule schedule = Schedule::Auto;
   int halo_passes = 0;      // passes per exchange with Sync (ghost depth m*K); 0 = auto
   Numerics numerics = Numerics::Fp32;
+  bool phase_timing = false;  // per-phase device times in RunStats (runs eagerly)
 };
 
 const char* init_mode_name(InitMode m);

@@ -47,6 +47,9 @@ struct RunStats {
   int64_t passes = 0;
   int64_t exchanges = 0;
   int64_t checks = 0;
+  // Per-phase time (Params::phase_timing; device event time on the GPU,
+  // summed over launches, so concurrent phases may add up to > seconds).
+  double t_exchange = 0.0, t_compute = 0.0, t_reduce = 0.0;
 };
 
 class Solver {
@@ -157,6 +160,31 @@ class Solver {
   };
   std::map<std::tuple<int64_t, bool, int, int64_t, int64_t>, GraphEntry> graphs_;
   bool capturing_ = false;
+
+  // Phase timing (eager runs only).
+  enum Phase { kExchange = 0, kCompute = 1, kReduce = 2 };
+  struct Span {
+    int phase;
+    hipEvent_t a, b;
+    double ha, hb;
+  };
+  class PhaseScope {
+   public:
+    PhaseScope(Solver* s, int phase, hipStream_t st);
+    ~PhaseScope();
+   private:
+    Solver* s_;
+    hipStream_t st_;
+    int idx_ = -1;
+  };
+  hipEvent_t pooled_event();
+  void flush_spans();
+  double phase_acc_[3] = {0, 0, 0};
+  int open_spans_ = 0;
+  std::vector<Span> spans_;
+  std::vector<hipEvent_t> event_pool_;
+  size_t pool_used_ = 0;
+  bool timing_ = false;
 };
 
 }  // namespace heat

@@ -85,6 +85,7 @@ Params params_from_c(const heat_params* p) {
   P.schedule = Schedule(p->schedule);
   P.halo_passes = p->halo_passes;
   P.numerics = Numerics(p->numerics);
+  P.phase_timing = p->phase_timing != 0;
   return P;
 }
 
@@ -213,6 +214,9 @@ int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out) {
       out->converged_at = r.converged_at;
       out->last_resid = r.last_resid;
       out->seconds = r.seconds;
+      out->t_exchange = r.t_exchange;
+      out->t_compute = r.t_compute;
+      out->t_reduce = r.t_reduce;
       out->passes = r.passes;
       out->exchanges = r.exchanges;
       out->checks = r.checks;

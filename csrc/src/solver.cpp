@@ -93,6 +93,7 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
     sched_ = Schedule::Sync;
   L_ = Layout::make(blk_.lx, blk_.ly, H_);
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
+  timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
   alloc();
   init_fields();
 }
@@ -168,6 +169,8 @@ void Solver::free_all() {
     if (d_checksum_) (void)hipFree(d_checksum_);
     for (auto e : {ev_ready_, ev_halo_, ev_t0_, ev_t1_})
       if (e) (void)hipEventDestroy(e);
+    for (auto e : event_pool_) (void)hipEventDestroy(e);
+    event_pool_.clear();
     if (s_comp_) (void)hipStreamDestroy(s_comp_);
     if (s_comm_) (void)hipStreamDestroy(s_comm_);
   } else {
@@ -216,6 +219,7 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
 // ---------------------------------------------------------------------------
 void Solver::exchange(int buf, int k, hipStream_t st) {
   TraceRange trace("heat.exchange");
+  PhaseScope phase(this, kExchange, st);
   float* f = field_[buf];
   const auto& nb = blk_.nbr;
   const int64_t lx = blk_.lx, ly = blk_.ly, pitch = L_.pitch;
@@ -290,6 +294,7 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
 // ---------------------------------------------------------------------------
 void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int64_t er,
                          int64_t ec) {
+  PhaseScope phase(this, kCompute, s_comp_);
   const float* src = field_[cur_];
   float* dst = field_[cur_ ^ 1];
   gpu::StencilGeom g;
@@ -346,6 +351,7 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
 }
 
 void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
+  PhaseScope phase(this, kCompute, nullptr);
   cpu::Geom g;
   g.pitch = L_.pitch;
   g.gx0 = blk_.ox;
@@ -451,6 +457,7 @@ void Solver::enqueue_pass(int k, bool resid) {
     }
     if (tb) cur_ ^= 1;
     if (resid) {
+      PhaseScope phase(this, kReduce, s_comp_);
       if (tr_->device_memory()) tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
       HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
     }
@@ -484,10 +491,61 @@ float Solver::finish_resid() {
     std::memcpy(&r, h_resid_, 4);
     if (!tr_->device_memory()) tr_->allreduce_max(&r, 1, nullptr);
   } else {
+    PhaseScope phase(this, kReduce, nullptr);
     r = cpu_resid_;
     tr_->allreduce_max(&r, 1, nullptr);
   }
   return r;
+}
+
+// ---------------------------------------------------------------------------
+// phase timing
+// ---------------------------------------------------------------------------
+hipEvent_t Solver::pooled_event() {
+  if (pool_used_ == event_pool_.size()) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    event_pool_.push_back(e);
+  }
+  return event_pool_[pool_used_++];
+}
+
+void Solver::flush_spans() {
+  synchronize();
+  for (const Span& sp : spans_) {
+    double dt = sp.hb - sp.ha;
+    if (sp.a) {
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, sp.a, sp.b));
+      dt = 1e-3 * double(ms);
+    }
+    phase_acc_[sp.phase] += dt;
+  }
+  spans_.clear();
+  pool_used_ = 0;
+}
+
+Solver::PhaseScope::PhaseScope(Solver* s, int phase, hipStream_t st) : s_(s), st_(st) {
+  if (!s_->timing_ || s_->capturing_) return;
+  // Bound the event pool on long runs (only between scopes: no open span).
+  if (s_->spans_.size() >= 4096 && s_->open_spans_ == 0) s_->flush_spans();
+  ++s_->open_spans_;
+  Span sp{phase, nullptr, nullptr, now_s(), 0.0};
+  if (s_->on_gpu() && st_) {
+    sp.a = s_->pooled_event();
+    sp.b = s_->pooled_event();
+    HIP_CHECK(hipEventRecord(sp.a, st_));
+  }
+  idx_ = int(s_->spans_.size());
+  s_->spans_.push_back(sp);
+}
+
+Solver::PhaseScope::~PhaseScope() {
+  if (idx_ < 0) return;
+  --s_->open_spans_;
+  Span& sp = s_->spans_[size_t(idx_)];
+  sp.hb = now_s();
+  if (sp.b) (void)hipEventRecord(sp.b, st_);
 }
 
 bool Solver::is_check_point(int64_t completed) const {
@@ -511,9 +569,14 @@ RunStats Solver::run(int64_t steps) {
   synchronize();
   const double t0 = now_s();
   const bool gpu = on_gpu();
-  const bool can_graph = gpu && P_.use_graph && !staged_ &&
+  const bool can_graph = gpu && P_.use_graph && !staged_ && !timing_ &&
                          (tr_->world() == 1 || tr_->graph_capturable()) &&
                          env_int("HEAT_GRAPH", 1) != 0;
+  if (timing_) {
+    spans_.clear();
+    pool_used_ = 0;
+    phase_acc_[0] = phase_acc_[1] = phase_acc_[2] = 0.0;
+  }
   if (can_graph && tr_->world() > 1 && !warmed_) {
     // Let RCCL establish its connections outside of stream capture.  A halo
     // exchange of the current buffer is idempotent.
@@ -600,6 +663,12 @@ RunStats Solver::run(int64_t steps) {
   synchronize();
   tr_->check();
   s.seconds = now_s() - t0;
+  if (timing_) {
+    flush_spans();
+    s.t_exchange = phase_acc_[kExchange];
+    s.t_compute = phase_acc_[kCompute];
+    s.t_reduce = phase_acc_[kReduce];
+  }
   s.total_steps = step_;
   s.passes = stat_passes_ - p0;
   s.exchanges = stat_exchanges_ - e0;

@@ -50,7 +50,7 @@ class HeatParams(Structure):
         ("use_graph", c_int32), ("overlap", c_int32),
         ("compat", c_int32), ("device", c_int32),
         ("schedule", c_int32), ("halo_passes", c_int32),
-        ("numerics", c_int32), ("pad_", c_int32),
+        ("numerics", c_int32), ("phase_timing", c_int32),
     ]
 
 
@@ -80,6 +80,7 @@ class HeatRunStats(Structure):
         ("converged", c_int32), ("converged_at", c_int64),
         ("last_resid", c_float), ("seconds", c_double),
         ("passes", c_int64), ("exchanges", c_int64), ("checks", c_int64),
+        ("t_exchange", c_double), ("t_compute", c_double), ("t_reduce", c_double),
     ]
 
 

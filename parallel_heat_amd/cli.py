@@ -53,6 +53,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--schedule", choices=["auto", "sync", "overlap", "pipeline"], default="auto")
     a("--halo-passes", type=int, default=0)
     a("--numerics", choices=["fp32", "mpi"], default="fp32")
+    a("--phase-timing", action="store_true")
     a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
@@ -71,7 +72,8 @@ def main(argv=None) -> int:
                      tb_depth=args.tb_depth, threads=args.threads, decomp=args.decomp,
                      px=args.px, py=args.py, use_graph=not args.no_graph,
                      overlap=not args.no_overlap, compat=compat, schedule=args.schedule,
-                     halo_passes=args.halo_passes, numerics=args.numerics)
+                     halo_passes=args.halo_passes, numerics=args.numerics,
+                     phase_timing=args.phase_timing)
     info = pcomm.init_distributed("nccl" if backend == "hip" else "gloo")
     root = info.is_root
     out = sys.stdout
@@ -111,7 +113,8 @@ def main(argv=None) -> int:
         emit(init_path)
     total = cfg.total_steps()
     todo = total - solver.step
-    acc = dict(steps_done=0, seconds=0.0, passes=0, exchanges=0, checks=0)
+    acc = dict(steps_done=0, seconds=0.0, passes=0, exchanges=0, checks=0, t_exchange=0.0,
+               t_compute=0.0, t_reduce=0.0)
     converged, converged_at, last = False, -1, -1.0
     while todo > 0:
         chunk = min(args.checkpoint_every, todo) if args.checkpoint_every > 0 else todo
@@ -141,7 +144,10 @@ def main(argv=None) -> int:
                 s_per_1000_iters=acc["seconds"] * 1000 / max(1, acc["steps_done"]),
                 converged=converged, converged_at=converged_at, last_resid=last,
                 passes=acc["passes"], exchanges=acc["exchanges"],
-                transport=solver.transport, native=_native.loaded_path()) + "\n")
+                transport=solver.transport, schedule=solver.info.schedule,
+                halo=solver.info.halo, t_exchange=acc["t_exchange"],
+                t_compute=acc["t_compute"], t_reduce=acc["t_reduce"],
+                native=_native.loaded_path()) + "\n")
         out.flush()
     solver.barrier()
     solver.close()

@@ -47,6 +47,7 @@ class HeatConfig:
     schedule: str = "auto"        # multi-rank pass schedule: auto(=sync) | sync | overlap | pipeline
     halo_passes: int = 0          # sync: passes per halo exchange (ghost depth m*K); 0 = auto
     numerics: str = "fp32"        # fp32 (canonical FMA) | mpi (reference MPI double arithmetic)
+    phase_timing: bool = False    # per-phase times (exchange/compute/reduce) in RunResult; eager
 
     def replace(self, **kw) -> "HeatConfig":
         return dataclasses.replace(self, **kw)
@@ -91,4 +92,5 @@ class HeatConfig:
         p.schedule = SCHEDULES[self.schedule]
         p.halo_passes = int(self.halo_passes)
         p.numerics = NUMERICS[self.numerics]
+        p.phase_timing = int(bool(self.phase_timing))
         return p

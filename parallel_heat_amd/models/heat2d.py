@@ -36,6 +36,9 @@ class RunResult:
     exchanges: int
     checks: int
     cells: int  # nx*ny
+    t_exchange: float = 0.0  # seconds in halo exchanges (phase_timing)
+    t_compute: float = 0.0   # seconds in stencil kernels
+    t_reduce: float = 0.0    # seconds in residual all-reduce + read-back
 
     @property
     def mcells_per_s(self) -> float:
@@ -162,7 +165,8 @@ class HeatSolver:
         _native.call("heat_solver_run", self._h, int(steps), ctypes.byref(st))
         return RunResult(st.steps_done, st.total_steps, bool(st.converged), st.converged_at,
                          st.last_resid, st.seconds, st.passes, st.exchanges, st.checks,
-                         self.config.nx * self.config.ny)
+                         self.config.nx * self.config.ny, st.t_exchange, st.t_compute,
+                         st.t_reduce)
 
     def reset(self) -> None:
         _native.call("heat_solver_reset", self._h)

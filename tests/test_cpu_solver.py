@@ -172,3 +172,15 @@ def test_mpi_numerics_decomposition_invariance(tmp_path, world):
     res = run_world(world, kw, 25, tmp_path)
     ref, _, _ = R.run_np(40, 36, 25, init="random", seed=5, numerics="mpi")
     assert np.array_equal(res["grid"], ref)
+
+
+def test_phase_timing_cpu(tmp_path):
+    cfg = HeatConfig(nx=64, ny=64, steps=40, converge=True, check_interval=10, backend="cpu",
+                     phase_timing=True)
+    with HeatSolver(cfg) as s:
+        r = s.run()
+    assert r.t_compute > 0 and r.t_exchange == 0 and r.t_reduce >= 0
+    assert r.t_compute <= r.seconds * 1.05 + 1e-3
+    from .dist_worker import run_world
+    res = run_world(2, dict(nx=40, ny=30, steps=0, backend="cpu", phase_timing=True), 12, tmp_path)
+    assert int(res["done"]) == 12

@@ -85,3 +85,31 @@ def test_loopback_scatter_and_naive_kernel(gpu):
         s.run(20)
         want = s.gather()
     assert np.array_equal(next(g for g in res if g is not None), want)
+
+
+def test_cli_single_process_gpus(gpu, tmp_path):
+    # `heat --gpus N`: one process, N ranks as threads (loopback transport).
+    import json
+    import subprocess
+
+    from parallel_heat_amd import _native
+    outs = {}
+    for n in (1, 3):
+        d = tmp_path / f"g{n}"
+        d.mkdir()
+        p = subprocess.run([str(_native.CLI_PATH), "--backend", "hip", "--gpus", str(n),
+                            "--nx", "130", "--ny", "90", "--steps", "37", "--init", "random",
+                            "--out", "c.json", "--out-format", "checksum", "--json"],
+                           cwd=d, capture_output=True, text=True, timeout=300, check=True)
+        outs[n] = (json.loads((d / "c.json").read_text()), json.loads(p.stdout.splitlines()[-1]))
+    assert outs[3][0]["hash"] == outs[1][0]["hash"]
+    assert outs[3][1]["ranks"] == 3 and outs[3][1]["transport"] == "loopback"
+
+
+def test_loopback_phase_timing(gpu):
+    cfg = HeatConfig(**{**BASE, "decomp": "rows", "phase_timing": True, "converge": True,
+                        "check_interval": 16})
+    res = run_group(cfg, 2, lambda s: s.run(64))
+    for r in res:
+        assert r.t_compute > 0 and r.t_exchange > 0 and r.t_reduce > 0
+        assert r.checks == 4
