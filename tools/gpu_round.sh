@@ -16,7 +16,7 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   cat gpurun_out/bench.log
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
-  cd /tmp && run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OLDPWD/gpurun_out/prof -o run -- python3 $OLDPWD/bench.py --steps 2 --warmup 1 > $OLDPWD/gpurun_out/prof.log 2>&1 || { tail -30 $OLDPWD/gpurun_out/prof.log; exit 1; }
+  cd /tmp && run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OLDPWD/gpurun_out/prof -o run -- python3 $OLDPWD/bench.py --steps 2 --warmup 1 > $OLDPWD/gpurun_out/prof.log 2>&1 || { tail -30 $OLDPWD/gpurun_out/prof.log; exit 1; }
   cd $OLDPWD
   find gpurun_out/prof -name "*stats*" | head
 fi
