@@ -59,6 +59,11 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 // skew 2; 2: 2-row rings + copy; 3: 3-row rings + ramp skip), bit 2
 // scalar-update build; -1 = default
 // (HEAT_TB_VARIANT or the tuned choice).
+// One Jacobi step over `box` from an LDS-staged 32x256 halo tile per
+// workgroup (float4 lanes, DPP east/west); honours g.numerics.
+void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
+              unsigned* resid, hipStream_t st);
+
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 int tb_default_variant();

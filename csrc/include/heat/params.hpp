@@ -29,6 +29,7 @@ enum class KernelKind : int {
   Auto = 0,   // temporally blocked streaming kernel (TB) at the tuned depth
   Naive = 1,  // one cell per thread, global loads only (independent oracle)
   TB = 2,     // register-streaming temporally blocked kernel, depth tb_depth
+  Lds = 3,    // LDS-staged halo tile, one step per launch (also --numerics mpi)
 };
 
 // Reference-compatibility switches.

@@ -76,6 +76,10 @@ class Solver {
   Schedule schedule() const { return sched_; }
   int tb_depth() const { return T_; }
   bool on_gpu() const { return P_.backend == Backend::Hip; }
+  // The temporally blocked kernel runs the passes (else k single-step launches).
+  bool tb_kernel() const {
+    return on_gpu() && (P_.kernel == KernelKind::Auto || P_.kernel == KernelKind::TB);
+  }
 
   // Re-initialise both fields from the initial condition (step := 0).
   void reset();

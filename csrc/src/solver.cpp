@@ -45,11 +45,11 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   if (on_gpu()) {
     // The TB kernel evaluates the canonical fp32 expression only.
     if (P_.numerics != Numerics::Fp32) {
-      HEAT_CHECK(P_.kernel != KernelKind::TB, "--numerics %s needs the naive kernel",
+      HEAT_CHECK(P_.kernel != KernelKind::TB, "--numerics %s needs the lds or naive kernel",
                  numerics_name(P_.numerics));
-      P_.kernel = KernelKind::Naive;
+      if (P_.kernel == KernelKind::Auto) P_.kernel = KernelKind::Lds;
     }
-    if (P_.kernel == KernelKind::Naive) {
+    if (!tb_kernel()) {
       T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
     } else {
       T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 8);
@@ -71,7 +71,7 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   }
   const int64_t min_ext = std::min(cart_.px > 1 ? min_lx : INT64_MAX, cart_.py > 1 ? min_ly : INT64_MAX);
   sched_ = P_.schedule == Schedule::Auto ? Schedule::Sync : P_.schedule;
-  if (!on_gpu() || P_.kernel == KernelKind::Naive || world == 1 || !P_.overlap)
+  if (!tb_kernel() || world == 1 || !P_.overlap)
     sched_ = Schedule::Sync;
   // Ghost depth H = m*T: with the Sync schedule one exchange feeds m passes,
   // each computing the still-valid part of the ghost ring redundantly.
@@ -203,7 +203,7 @@ int64_t Solver::configured_steps(int64_t steps) const {
 
 std::vector<int> Solver::pass_depths(int64_t n) const {
   std::vector<int> d;
-  const bool tb = on_gpu() && P_.kernel != KernelKind::Naive;
+  const bool tb = tb_kernel();
   while (n > 0) {
     int k = int(std::min<int64_t>(T_, n));
     if (tb)
@@ -315,7 +315,7 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
   const Box own{nb[North] >= 0 ? -er : 0, lx + (nb[South] >= 0 ? er : 0),
                 nb[West] >= 0 ? -ec : 0, ly + (nb[East] >= 0 ? ec : 0)};
 
-  if (P_.kernel == KernelKind::Naive) {
+  if (!tb_kernel()) {
     // k single steps over shrinking regions (deep halo), ping-ponging.
     for (int j = 0; j < k; ++j) {
       const int64_t e = k - 1 - j;
@@ -323,7 +323,10 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
             nb[West] >= 0 ? own.c0 - e : 0, own.c1 + (nb[East] >= 0 ? e : 0)};
       const float* a = field_[cur_];
       float* d = field_[cur_ ^ 1];
-      gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+      if (P_.kernel == KernelKind::Lds)
+        gpu::lds_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+      else
+        gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
       cur_ ^= 1;
     }
     return;
@@ -385,7 +388,7 @@ std::pair<int64_t, int64_t> Solver::ensure_ghosts(int k, hipStream_t st) {
     gr_ = gc_ = H_;
   }
   // TB boxes start on a float4 column: round the column extension down.
-  const bool tb = on_gpu() && P_.kernel != KernelKind::Naive;
+  const bool tb = tb_kernel();
   const int64_t er = ns ? gr_ - k : 0;
   const int64_t ec = ew ? (tb ? round_down(gc_ - k, 4) : gc_ - k) : 0;
   gr_ = er;
@@ -399,7 +402,7 @@ void Solver::enqueue_pass(int k, bool resid) {
   const bool multi = tr_->world() > 1;
   if (on_gpu()) {
     if (resid) HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
-    const bool tb = P_.kernel != KernelKind::Naive;
+    const bool tb = tb_kernel();
     const int64_t lx = blk_.lx, ly = blk_.ly;
     const int band = sched_ == Schedule::Pipeline ? H_ : k;
     const int64_t ir0 = nb[North] >= 0 ? band : 0, ir1 = nb[South] >= 0 ? lx - band : lx;

@@ -117,6 +117,22 @@ def naive_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
                  ctypes.c_void_p(_stream()))
 
 
+def lds_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
+             resid: Optional[torch.Tensor] = None, numerics: str = "fp32") -> None:
+    """One Jacobi step over `box` with the LDS-staged tile kernel (GPU only);
+    numerics "fp32" (canonical FMA) or "mpi" (reference MPI double arithmetic)."""
+    r0, r1, c0, c1 = box or (0, src.lx, 0, src.ly)
+    if src.pitch != dst.pitch:
+        raise ValueError("src/dst layouts differ")
+    if src.device.type != "cuda":
+        raise ValueError("lds_step needs GPU fields")
+    rp = _resid_ptr(resid)
+    _native.call("heat_op_lds_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
+                 src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy,
+                 r0, r1, c0, c1, ctypes.c_void_p(rp) if rp else None,
+                 ctypes.c_void_p(_stream()), {"fp32": 0, "mpi": 1}[numerics])
+
+
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
             waves_target: int = 0, variant: int = -1) -> None:

@@ -28,7 +28,8 @@ def grid_of(results):
 @pytest.mark.parametrize("schedule", ["sync", "overlap", "pipeline"])
 @pytest.mark.parametrize("world,kw", [(2, dict(decomp="rows")), (2, dict(px=1, py=2)),
                                       (4, dict(decomp="auto")), (3, dict(decomp="rows")),
-                                      (6, dict(decomp="auto"))])
+                                      (6, dict(decomp="auto")),
+                                      (4, dict(decomp="auto", kernel="lds", tb_depth=3))])
 def test_loopback_schedules(gpu, world, kw, schedule):
     cfg = HeatConfig(**{**BASE, **kw, "schedule": schedule})
     def fn(s):

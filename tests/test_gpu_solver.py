@@ -16,7 +16,7 @@ def _run(cfg, steps=None):
 
 
 @pytest.mark.parametrize("kernel,depth", [("naive", 1), ("naive", 3), ("tb", 1), ("tb", 5),
-                                          ("tb", 8), ("tb", 7)])
+                                          ("tb", 8), ("tb", 7), ("lds", 1), ("lds", 4)])
 @pytest.mark.parametrize("graph", [True, False])
 def test_gpu_equals_cpu(gpu, kernel, depth, graph):
     cfg = HeatConfig(nx=150, ny=333, steps=45, init="random", seed=9, backend="hip",
