@@ -36,7 +36,7 @@ void usage() {
       "  --eps F                 convergence threshold on max|delta|    [1e-3]\n"
       "  --backend cpu|hip       compute backend                        [hip if a GPU exists]\n"
       "  --threads N             CPU OpenMP threads                     [runtime default]\n"
-      "  --kernel auto|tb|lds|naive  GPU kernel family (auto = tb)       [auto]\n"
+      "  --kernel auto|tb|lds|mfma|naive  GPU kernel family (auto = tb)  [auto]\n"
       "  --tb-depth K            fused steps per pass (= halo depth)    [8 hip, 1 cpu]\n"
       "  --decomp auto|rows|2d   process grid (auto = MPI_Dims_create)  [auto]\n"
       "  --px P --py Q           explicit process grid\n"
@@ -250,6 +250,7 @@ int main(int argc, char** argv) {
       P.kernel = k == "naive" ? KernelKind::Naive
                  : k == "tb"  ? KernelKind::TB
                  : k == "lds" ? KernelKind::Lds
+                 : k == "mfma" ? KernelKind::Mfma
                               : KernelKind::Auto;
     } else if (a == "--tb-depth") P.tb_depth = std::atoi(need().c_str());
     else if (a == "--decomp") {

@@ -131,6 +131,9 @@ int heat_op_naive_step(const float* src, float* dst, int64_t pitch, int64_t gx0,
 int heat_op_lds_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                      int64_t nx, int64_t ny, float cx, float cy, int64_t r0, int64_t r1,
                      int64_t c0, int64_t c1, unsigned* resid, void* stream, int numerics);
+int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
+                      int64_t nx, int64_t ny, float cx, float cy, int64_t r0, int64_t r1,
+                      int64_t c0, int64_t c1, unsigned* resid, void* stream);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,

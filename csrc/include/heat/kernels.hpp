@@ -64,6 +64,11 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
               unsigned* resid, hipStream_t st);
 
+// One Jacobi step over `box` as banded matrix products on the fp32 MFMA
+// units (v_mfma_f32_16x16x4_f32); rounding differs from heat::stencil.
+void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
+               unsigned* resid, hipStream_t st);
+
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 int tb_default_variant();

@@ -30,6 +30,8 @@ enum class KernelKind : int {
   Naive = 1,  // one cell per thread, global loads only (independent oracle)
   TB = 2,     // register-streaming temporally blocked kernel, depth tb_depth
   Lds = 3,    // LDS-staged halo tile, one step per launch (also --numerics mpi)
+  Mfma = 4,   // the stencil as banded matmuls on fp32 MFMA, one step per launch
+              // (an experiment: not bitwise equal to the others; see mfma.hip)
 };
 
 // Reference-compatibility switches.

@@ -31,6 +31,7 @@ const char* kernel_name(KernelKind k) {
     case KernelKind::Naive: return "naive";
     case KernelKind::TB: return "tb";
     case KernelKind::Lds: return "lds";
+    case KernelKind::Mfma: return "mfma";
   }
   return "?";
 }
@@ -370,6 +371,15 @@ int heat_op_lds_step(const float* src, float* dst, int64_t pitch, int64_t gx0, i
     auto g = geom(pitch, gx0, gy0, nx, ny, cx, cy);
     g.numerics = numerics;
     heat::gpu::lds_step(src, dst, g, heat::Box{r0, r1, c0, c1}, resid, S(stream));
+  });
+}
+
+int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
+                      int64_t nx, int64_t ny, float cx, float cy, int64_t r0, int64_t r1,
+                      int64_t c0, int64_t c1, unsigned* resid, void* stream) {
+  return guard([&] {
+    heat::gpu::mfma_step(src, dst, geom(pitch, gx0, gy0, nx, ny, cx, cy),
+                         heat::Box{r0, r1, c0, c1}, resid, S(stream));
   });
 }
 

@@ -45,8 +45,8 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   if (on_gpu()) {
     // The TB kernel evaluates the canonical fp32 expression only.
     if (P_.numerics != Numerics::Fp32) {
-      HEAT_CHECK(P_.kernel != KernelKind::TB, "--numerics %s needs the lds or naive kernel",
-                 numerics_name(P_.numerics));
+      HEAT_CHECK(P_.kernel != KernelKind::TB && P_.kernel != KernelKind::Mfma,
+                 "--numerics %s needs the lds or naive kernel", numerics_name(P_.numerics));
       if (P_.kernel == KernelKind::Auto) P_.kernel = KernelKind::Lds;
     }
     if (!tb_kernel()) {
@@ -325,6 +325,8 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
       float* d = field_[cur_ ^ 1];
       if (P_.kernel == KernelKind::Lds)
         gpu::lds_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+      else if (P_.kernel == KernelKind::Mfma)
+        gpu::mfma_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
       else
         gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
       cur_ ^= 1;

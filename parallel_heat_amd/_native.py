@@ -140,6 +140,9 @@ _SIGS = {
     "heat_op_lds_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64,
                                  c_int64, c_float, c_float, c_int64, c_int64, c_int64, c_int64,
                                  c_void_p, c_void_p, c_int]),
+    "heat_op_mfma_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64,
+                                  c_int64, c_float, c_float, c_int64, c_int64, c_int64, c_int64,
+                                  c_void_p, c_void_p]),
     "heat_op_tb_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                 c_float, c_float, POINTER(c_int64), c_int, c_int, c_void_p,
                                 c_void_p, c_int, c_int]),

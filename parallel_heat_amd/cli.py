@@ -36,7 +36,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--eps", type=float, default=1e-3)
     a("--backend", choices=["cpu", "hip"], default=None)
     a("--threads", type=int, default=0)
-    a("--kernel", choices=["auto", "naive", "tb", "lds"], default="auto")
+    a("--kernel", choices=["auto", "naive", "tb", "lds", "mfma"], default="auto")
     a("--tb-depth", type=int, default=0)
     a("--decomp", choices=["auto", "rows", "1d", "2d"], default="auto")
     a("--px", type=int, default=0)

@@ -14,7 +14,7 @@ from .. import _native
 
 INIT_MODES = {"ref-wrap": 0, "exact": 1, "ref64": 1, "random": 2, "zero": 3}
 BACKENDS = {"cpu": 0, "hip": 1}
-KERNELS = {"auto": 0, "naive": 1, "tb": 2, "lds": 3}
+KERNELS = {"auto": 0, "naive": 1, "tb": 2, "lds": 3, "mfma": 4}
 DECOMPS = {"auto": 0, "rows": 1, "1d": 1, "2d": 2}
 COMPATS = {"none": 0, "mpi": 1, "cuda": 2}
 SCHEDULES = {"auto": 0, "sync": 1, "overlap": 2, "pipeline": 3}

@@ -133,6 +133,22 @@ def lds_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
                  ctypes.c_void_p(_stream()), {"fp32": 0, "mpi": 1}[numerics])
 
 
+def mfma_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
+              resid: Optional[torch.Tensor] = None) -> None:
+    """One Jacobi step over `box` as banded matmuls on the fp32 MFMA units
+    (GPU only; rounding differs from the canonical expression by ~1 ulp)."""
+    r0, r1, c0, c1 = box or (0, src.lx, 0, src.ly)
+    if src.pitch != dst.pitch:
+        raise ValueError("src/dst layouts differ")
+    if src.device.type != "cuda":
+        raise ValueError("mfma_step needs GPU fields")
+    rp = _resid_ptr(resid)
+    _native.call("heat_op_mfma_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
+                 src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy,
+                 r0, r1, c0, c1, ctypes.c_void_p(rp) if rp else None,
+                 ctypes.c_void_p(_stream()))
+
+
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
             waves_target: int = 0, variant: int = -1) -> None:

@@ -154,3 +154,30 @@ def test_lds_step_mpi_numerics(gpu):
     ops.lds_step(a, b, g, numerics="mpi")
     torch.cuda.synchronize()
     assert np.array_equal(b.owned().cpu().numpy(), R.step_np_mpi(u0))
+
+
+def test_mfma_step_close_to_oracle(gpu):
+    lx, ly = 203, 517
+    g, a, b = _fields(lx, ly, 4, gpu)
+    r = torch.zeros(4, dtype=torch.int32, device=gpu)
+    ops.mfma_step(a, b, g, resid=r)
+    torch.cuda.synchronize()
+    ref = _cpu_steps(g, lx, ly, 4, 1)
+    got = b.owned().cpu()
+    # exact fp32 products, different association than heat::stencil
+    assert (got - ref).abs().max() <= 2e-5
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[:, -1], ref[:, -1])  # ring fixed
+    assert abs(ops.resid_value(r) - float((got - a.owned().cpu()).abs().max())) == 0.0
+
+
+def test_mfma_step_tiling_invariance(gpu):
+    # Every cell gets the same fmaf chain wherever it falls in a 16x16 tile.
+    lx, ly = 150, 300
+    g, a, b1 = _fields(lx, ly, 4, gpu)
+    b2 = ops.Field(lx, ly, 4, gpu)
+    ops.init_field(b2, g, "random", 3)
+    ops.mfma_step(a, b1, g)
+    for box in [(0, 37, 0, 101), (0, 37, 101, ly), (37, lx, 0, 5), (37, lx, 5, ly)]:
+        ops.mfma_step(a, b2, g, box)
+    torch.cuda.synchronize()
+    assert torch.equal(b1.owned(), b2.owned())

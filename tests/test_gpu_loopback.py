@@ -114,3 +114,19 @@ def test_loopback_phase_timing(gpu):
     for r in res:
         assert r.t_compute > 0 and r.t_exchange > 0 and r.t_reduce > 0
         assert r.checks == 4
+
+
+def test_loopback_mfma_kernel_invariance(gpu):
+    cfg = HeatConfig(**{**BASE, "decomp": "auto", "kernel": "mfma", "tb_depth": 4})
+
+    def fn(s):
+        s.run(21)
+        return s.gather()
+
+    res = run_group(cfg, 4, fn)
+    with HeatSolver(cfg.replace(decomp="auto")) as s:
+        s.run(21)
+        want = s.gather()
+    assert np.array_equal(next(g for g in res if g is not None), want)
+    ref, _, _ = single(cfg.replace(kernel="tb", tb_depth=8), 21)
+    assert np.abs(want - ref).max() <= 1e-3

@@ -32,6 +32,7 @@ def main():
         "naive": lambda s, d: ops.naive_step(s, d, g),
         "lds_fp32": lambda s, d: ops.lds_step(s, d, g),
         "lds_mpi": lambda s, d: ops.lds_step(s, d, g, numerics="mpi"),
+        "mfma": lambda s, d: ops.mfma_step(s, d, g),
         "tb8": None,
     }
     res = {k: [] for k in kinds}
