@@ -95,6 +95,8 @@ int heat_device_count(int* n);
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out);
 int heat_solver_destroy(heat_solver* s);
 int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
+/* RCCL on one rank: self send/recv (eager or hipGraph-captured) + all-reduce. */
+int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double* gbps);
 /* Loopback transport: ranks are threads of this process sharing one hub. */
 int heat_loopback_hub_create(int world, void** out);
 int heat_loopback_hub_destroy(void* hub);

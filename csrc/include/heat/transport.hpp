@@ -73,6 +73,9 @@ std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const void* 
                                                int device);
 // Writes a fresh ncclUniqueId (128 bytes) into out.
 void rccl_unique_id(void* out128);
+// Single-rank RCCL check on `device`: self send/recv of `bytes` (eager or in
+// a captured hipGraph) and an all-reduce; throws on wrong data, returns GB/s.
+double rccl_self_test(int device, size_t bytes, bool graph, int iters);
 
 // TCP: rank 0 listens on (addr, port); everyone connects to everyone
 // (full mesh, one socket per peer pair).

@@ -149,6 +149,10 @@ int heat_device_count(int* n) {
   });
 }
 
+int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double* gbps) {
+  return guard([&] { *gbps = heat::rccl_self_test(device, size_t(bytes), graph != 0, iters); });
+}
+
 int heat_loopback_hub_create(int world, void** out) {
   return guard([&] { *out = heat::loopback_hub_create(world); });
 }

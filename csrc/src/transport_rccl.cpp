@@ -9,7 +9,9 @@
 // capture whole step chunks, exchanges included, into one hipGraph.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "heat/common.hpp"
 #include "heat/transport.hpp"
@@ -55,15 +57,13 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max(float* buf, int count, hipStream_t st) override {
-    if (world_ > 1) NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat, ncclMax, comm_, st));
+    NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat, ncclMax, comm_, st));
   }
   void allreduce_sum_f64(double* buf, int count, hipStream_t st) override {
-    if (world_ > 1)
-      NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat64, ncclSum, comm_, st));
+    NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat64, ncclSum, comm_, st));
   }
   void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) override {
-    if (world_ > 1)
-      NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclUint64, ncclSum, comm_, st));
+    NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclUint64, ncclSum, comm_, st));
   }
   void barrier() override {
     if (world_ == 1) return;
@@ -94,6 +94,70 @@ class RcclTransport final : public Transport {
 std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const void* unique_id,
                                                int device) {
   return std::make_unique<RcclTransport>(rank, world, unique_id, device);
+}
+
+double rccl_self_test(int device, size_t bytes, bool graph, int iters) {
+  // One-rank communicator; rank 0 sends to and receives from itself inside
+  // ncclGroupStart/End, eagerly or as a captured hipGraph, then a max
+  // all-reduce.  Checks the bytes and returns the achieved GB/s.
+  HIP_CHECK(hipSetDevice(device));
+  unsigned char uid[128];
+  rccl_unique_id(uid);
+  auto tr = make_rccl_transport(0, 1, uid, device);
+  const size_t n = std::max<size_t>(bytes / 4, 1);
+  float *a = nullptr, *b = nullptr;
+  HIP_CHECK(hipMalloc(&a, std::max<size_t>(n * 4, 256)));
+  HIP_CHECK(hipMalloc(&b, std::max<size_t>(n * 4, 256)));
+  std::vector<float> h(n), back(n);
+  for (size_t i = 0; i < n; ++i) h[i] = float(i % 9973) * 0.5f;
+  HIP_CHECK(hipMemcpy(a, h.data(), n * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemset(b, 0, n * 4));
+  hipStream_t st;
+  HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  Msg m{0, a, n * 4, b, n * 4};
+  hipGraphExec_t exec = nullptr;
+  if (graph) {
+    tr->sendrecv(&m, 1, st);  // connect outside capture
+    HIP_CHECK(hipStreamSynchronize(st));
+    HIP_CHECK(hipMemset(b, 0, n * 4));
+    hipGraph_t g;
+    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    tr->sendrecv(&m, 1, st);
+    HIP_CHECK(hipStreamEndCapture(st, &g));
+    HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+  }
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  HIP_CHECK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) {
+    if (exec) HIP_CHECK(hipGraphLaunch(exec, st));
+    else tr->sendrecv(&m, 1, st);
+  }
+  HIP_CHECK(hipEventRecord(e1, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  tr->check();
+  HIP_CHECK(hipMemcpy(back.data(), b, n * 4, hipMemcpyDeviceToHost));
+  const bool ok = std::memcmp(back.data(), h.data(), n * 4) == 0;
+  // all-reduces on one rank are the identity
+  tr->allreduce_max(a, 4, st);
+  tr->allreduce_sum_f64(reinterpret_cast<double*>(b), 2, st);
+  HIP_CHECK(hipStreamSynchronize(st));
+  float first[4];
+  HIP_CHECK(hipMemcpy(first, a, sizeof first, hipMemcpyDeviceToHost));
+  const bool ok_ar = std::memcmp(first, h.data(), std::min(n, size_t(4)) * 4) == 0;
+  if (exec) (void)hipGraphExecDestroy(exec);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  HEAT_CHECK(ok, "RCCL self send/recv delivered wrong bytes");
+  HEAT_CHECK(ok_ar, "RCCL all-reduce on one rank changed the data");
+  return double(bytes) * iters / (double(ms) * 1e-3) / 1e9;
 }
 
 void rccl_unique_id(void* out128) {

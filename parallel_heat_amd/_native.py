@@ -112,6 +112,7 @@ _SIGS = {
     "heat_solver_destroy": (c_int, [c_void_p]),
     "heat_solver_run": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
     "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "heat_rccl_self_test": (c_int, [c_int, c_int64, c_int, c_int, POINTER(c_double)]),
     "heat_loopback_hub_destroy": (c_int, [c_void_p]),
     "heat_solver_reset": (c_int, [c_void_p]),
     "heat_solver_info": (c_int, [c_void_p, POINTER(HeatBlockInfo)]),
