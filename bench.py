@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nx", type=int, default=8192)
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: nx rows PER GPU (the grid grows with N); not the headline")
     ap.add_argument("--ny", type=int, default=8192)
     ap.add_argument("--iters-per-step", type=int, default=1000)
     ap.add_argument("--tb-depth", type=int, default=0)
@@ -58,6 +60,8 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.weak:
+        args.nx *= world
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
               file=sys.stderr)
@@ -118,7 +122,7 @@ def main() -> int:
             "ms_per_step": round(ms_per_step, 4),
             "sec_per_1000_iters": round(elapsed * 1000.0 / max(1, done), 6),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": round(mcells / BASELINE_MCELLS, 3),
             "dtype": "fp32",
             "data": "synthetic (random-init temperature grid, seed 1234)",
