@@ -35,7 +35,10 @@ struct StencilGeom {
 constexpr int kTbMaxDepth = 8;  // deeper lost every sweep (register bound)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.
-int tb_strip_width(int k);
+// Output columns per TB strip (64 lanes x lane_cols, minus the overlap) and
+// the lane width of a variant (4: float4 lanes; variant bit 64: float2).
+int tb_strip_width(int k, int lane_cols = 4);
+int tb_lane_cols(int variant);
 
 // Fill every allocated cell (owned, ghost ring and padding) of a field with
 // the initial condition at its global coordinates (0 outside the plate).

@@ -105,7 +105,6 @@ class Solver {
   float* current() { return field_[cur_]; }
 
  private:
-  struct Plan;  // pass schedule of one segment
   void alloc();
   void free_all();
   void init_fields();
@@ -136,7 +135,6 @@ class Solver {
   bool comm_pending_ = false;  // comm stream has unjoined work
   int cur_ = 0;
   int64_t step_ = 0;
-  int64_t resid_pending_ = 0;
   float cpu_resid_ = 0.f;
   int64_t stat_passes_ = 0, stat_exchanges_ = 0;
 
@@ -151,7 +149,7 @@ class Solver {
 
   // GPU state.
   hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
-  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr;
+  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr;
   unsigned* d_resid_ = nullptr;
   float* h_resid_ = nullptr;
   void* d_scratch_ = nullptr;

@@ -161,7 +161,10 @@ bool tb_depth_supported(int k) {
   return k >= 1 && k <= kTbMaxDepth;
 }
 
-int tb_strip_width(int k) { return 256 - 2 * int(round_up(k, 4)); }
+int tb_strip_width(int k, int lane_cols) {
+  return 64 * lane_cols - 2 * int(round_up(k, lane_cols));
+}
+int tb_lane_cols(int variant) { return (variant & 64) ? 2 : 4; }
 
 int tb_variant_lag(int variant) {
   if ((variant & 3) == 3 && (variant & 8)) return 4;  // ramp + 6-row prefetch
@@ -219,7 +222,9 @@ int tb_resident_waves(int depth, int variant) {
   int cus = 0;
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int lag = tb_variant_lag(variant);
-  const int per_cu = (variant & 4) ? tbs::occupancy(depth, lag) : tbp::occupancy(depth, lag);
+  const int per_cu = (variant & 64)  ? tbn::occupancy(depth, lag)
+                     : (variant & 4) ? tbs::occupancy(depth, lag)
+                                     : tbp::occupancy(depth, lag);
   const int w = std::max(1, cus * std::max(1, per_cu) * 4);
   cache.emplace(key, w);
   return w;
@@ -257,7 +262,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   if (variant < 0) variant = tb_default_variant();
   const int lag = tb_variant_lag(variant);
-  const int W = tb_strip_width(depth);
+  const int W = tb_strip_width(depth, tb_lane_cols(variant));
   int64_t total_strip_rows = 0;
   for (int b = 0; b < nbox; ++b)
     if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
@@ -349,7 +354,9 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   if (n == 0) return;
   args.nbox = n;
   args.total_waves = waves;
-  const bool ok = (variant & 4) ? tbs::launch(args, depth, lag, st) : tbp::launch(args, depth, lag, st);
+  const bool ok = (variant & 64)  ? tbn::launch(args, depth, lag, st)
+                  : (variant & 4) ? tbs::launch(args, depth, lag, st)
+                                  : tbp::launch(args, depth, lag, st);
   HEAT_CHECK(ok, "unsupported TB depth %d", depth);
   HIP_CHECK(hipGetLastError());
 }

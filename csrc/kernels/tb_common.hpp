@@ -55,3 +55,7 @@ namespace heat::gpu::tbs {
 bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);
 int occupancy(int depth, int lag);
 }
+namespace heat::gpu::tbn {  // float2 lanes (tb_narrow.hip)
+bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);
+int occupancy(int depth, int lag);
+}

@@ -5,8 +5,9 @@
 // -fno-slp-vectorize: scalar row update).  The two builds exist so the row
 // update's instruction selection can be A/B-timed in one process.
 //
-// Structure (one wave = one 256-column strip x one chunk of rows):
-//   lane l holds columns [4l, 4l+4) of the strip as a float4;
+// Structure (one wave = one 64*V-column strip x one chunk of rows):
+//   lane l holds columns [Vl, Vl+V) of the strip as a float4 (V=4) or a
+//   float2 (V=2, the narrow-strip build tb_narrow.hip);
 //   level 0 = the input rows, level s = the field after s steps;
 //   every loop iteration loads one input row and advances every level by one
 //   row, keeping each level's last rows in a register ring;
@@ -22,8 +23,20 @@
 #ifndef HEAT_TB_NS
 #error "define HEAT_TB_NS"
 #endif
+// Columns per lane: 4 (float4, 256-column strips) or 2 (float2, 128-column
+// strips: twice the strips, so twice the chunk length at the same wave count
+// on small blocks, at 2x the relative strip overlap).
+#ifndef HEAT_TB_V
+#define HEAT_TB_V 4
+#endif
+#if HEAT_TB_PACKED && HEAT_TB_V != 4
+#error "the packed row update is written for float4 lanes"
+#endif
 
 namespace heat::gpu::HEAT_TB_NS {
+
+constexpr int V = HEAT_TB_V;
+typedef float vecf __attribute__((ext_vector_type(HEAT_TB_V)));
 
 using heat::gpu::tbdetail::TbArgs;
 using heat::gpu::tbdetail::TbBox;
@@ -49,14 +62,14 @@ constexpr int kModeGeneric = 6;
 template <int MODE>
 struct RowUpdate {
   float cx, cy;
-  bool cm0, cm1, cm2, cm3;  // MODE 6: per-column "updatable" masks; MODE 1-5: cm0 = this
-                            // lane holds the boundary column
-  __device__ __forceinline__ float4 operator()(const float4& a, const float4& b, const float4& c,
-                                               bool row_ok) const {
+  bool cm[V];  // MODE 6: per-column "updatable" masks; MODE 1-5: cm[0] = this
+               // lane holds the boundary column
+  __device__ __forceinline__ vecf operator()(const vecf& a, const vecf& b, const vecf& c,
+                                             bool row_ok) const {
+    vecf r;
+#if HEAT_TB_PACKED
     const float w = dpp_from_left(b.w);
     const float e = dpp_from_right(b.x);
-    float4 r;
-#if HEAT_TB_PACKED
     // Explicit pairs (x,y) and (z,w): v_pk_add_f32 / v_pk_fma_f32 on aligned
     // register pairs; the east+west sums are scalar adds (two of them fuse
     // the DPP lane shift) written straight into aligned pairs.
@@ -73,28 +86,24 @@ struct RowUpdate {
     const f2 ty23 = __builtin_elementwise_fma(m2, b23, ew23);
     const f2 r01 = __builtin_elementwise_fma(cy2, ty01, __builtin_elementwise_fma(cx2, tx01, b01));
     const f2 r23 = __builtin_elementwise_fma(cy2, ty23, __builtin_elementwise_fma(cx2, tx23, b23));
-    r = make_float4(r01.x, r01.y, r23.x, r23.y);
+    r = vecf{r01.x, r01.y, r23.x, r23.y};
 #else
-    r.x = stencil(b.x, a.x, c.x, w, b.y, cx, cy);
-    r.y = stencil(b.y, a.y, c.y, b.x, b.z, cx, cy);
-    r.z = stencil(b.z, a.z, c.z, b.y, b.w, cx, cy);
-    r.w = stencil(b.w, a.w, c.w, b.z, e, cx, cy);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float w = j == 0 ? dpp_from_left(b[V - 1]) : b[j - 1];
+      const float e = j == V - 1 ? dpp_from_right(b[0]) : b[j + 1];
+      r[j] = stencil(b[j], a[j], c[j], w, e, cx, cy);
+    }
 #endif
     if constexpr (MODE == kModeGeneric) {
       // Branch-free: keep b where the row (wave-uniform) or the column
       // (per lane) is not a global interior cell.
-      r.x = (cm0 && row_ok) ? r.x : b.x;
-      r.y = (cm1 && row_ok) ? r.y : b.y;
-      r.z = (cm2 && row_ok) ? r.z : b.z;
-      r.w = (cm3 && row_ok) ? r.w : b.w;
-    } else if constexpr (MODE == 1 || MODE == 2) {
-      r.x = cm0 ? b.x : r.x;  // one v_cndmask per row and level
-    } else if constexpr (MODE == 3) {
-      r.y = cm0 ? b.y : r.y;
-    } else if constexpr (MODE == 4) {
-      r.z = cm0 ? b.z : r.z;
-    } else if constexpr (MODE == 5) {
-      r.w = cm0 ? b.w : r.w;
+#pragma unroll
+      for (int j = 0; j < V; ++j) r[j] = (cm[j] && row_ok) ? r[j] : b[j];
+    } else if constexpr (MODE == 1) {
+      r[0] = cm[0] ? b[0] : r[0];  // one v_cndmask per row and level
+    } else if constexpr (MODE >= 2 && MODE - 2 < V) {
+      r[MODE - 2] = cm[0] ? b[MODE - 2] : r[MODE - 2];
     }
     return r;
   }
@@ -120,28 +129,27 @@ struct TbStream {
   static constexpr int PF = LAG == 4 ? 6 : RING;
   static constexpr int SKEW = LAG == 2 ? 2 : 1;
   static constexpr int STEP = LAG == 2 ? 2 : 1;  // row skew per level in the ring bodies
-  float4 R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
-  float4 P[PF];       // prefetch ring (input row i + PF)
+  vecf R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
+  vecf P[PF];       // prefetch ring (input row i + PF)
   unsigned m = 0;
-  int rc = 4;  // elements of this lane inside the box (the residual skips the rest)
+  int rc = V;  // elements of this lane inside the box (the residual skips the rest)
 
-  __device__ __forceinline__ void emit(const float4& out, const float4& b, int64_t ro,
+  __device__ __forceinline__ void emit(const vecf& out, const vecf& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
                                        int64_t re, bool store_lane, bool want_resid) {
     if (ro >= rb && ro < re && store_lane) {
-      *reinterpret_cast<float4*>(dst + ro * pitch) = out;
+      *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
       if (want_resid) {
         // Columns past the box end (the last lane's spill into padding or
         // stale ghost columns) are written but not part of the residual.
-        m = max(m, __float_as_uint(fabsf(out.x - b.x)));
-        m = max(m, rc > 1 ? __float_as_uint(fabsf(out.y - b.y)) : 0u);
-        m = max(m, rc > 2 ? __float_as_uint(fabsf(out.z - b.z)) : 0u);
-        m = max(m, rc > 3 ? __float_as_uint(fabsf(out.w - b.w)) : 0u);
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          m = max(m, (j == 0 || rc > j) ? __float_as_uint(fabsf(out[j] - b[j])) : 0u);
       }
     }
   }
 
-  template <int U, int V = U>
+  template <int U, int Q = U>
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int rlo, int rhi,
@@ -150,10 +158,10 @@ struct TbStream {
     if constexpr (LAG == 0) {
       // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
       // s holds rows i-s-2 (slot (U-s)&1) and i-s-1 (slot (U-s-1)&1).
-      float4 c = P[U];
+      vecf c = P[U];
       {
         const int64_t nxt = min(i + RING, last_in);
-        P[U] = *reinterpret_cast<const float4*>(src + nxt * pitch);
+        P[U] = *reinterpret_cast<const vecf*>(src + nxt * pitch);
       }
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -162,16 +170,16 @@ struct TbStream {
         const int sa = modn<2>(U - s), sb = modn<2>(U - s - 1);
         const int64_t row = i - s - 1;  // row of level s+1 computed now
         const bool ok = !ROWCHK || row_in(row, rlo, rhi);
-        const float4 cn = upd(R[s][sa], R[s][sb], c, ok);
+        const vecf cn = upd(R[s][sa], R[s][sb], c, ok);
         if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane, want_resid);
         R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
         c = cn;
       }
     } else {
-      R[0][U] = P[V];
+      R[0][U] = P[Q];
       {
         const int64_t nxt = min(i + PF, last_in);
-        P[V] = *reinterpret_cast<const float4*>(src + nxt * pitch);
+        P[Q] = *reinterpret_cast<const vecf*>(src + nxt * pitch);
       }
       // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
       // iterations, so the order below carries no dependency.
@@ -186,8 +194,8 @@ struct TbStream {
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
       const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
-      const float4& b = R[K - 1][modn<RING>(U - rK)];
-      const float4 out =
+      const vecf& b = R[K - 1][modn<RING>(U - rK)];
+      const vecf out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
       emit(out, b, ro, dst, pitch, rb, re, store_lane, want_resid);
     }
@@ -210,10 +218,10 @@ struct TbStream {
                                        int64_t pitch, int64_t last_in, int rlo, int rhi,
                                        const RowUpdate<MODE>& upd) {
     if constexpr (T < 2 * K) {
-      constexpr int U = T % 3, V = T % PF;
+      constexpr int U = T % 3, Q = T % PF;
       const int64_t i = first_in + T;
-      R[0][U] = P[V];
-      P[V] = *reinterpret_cast<const float4*>(src + min(i + PF, last_in) * pitch);
+      R[0][U] = P[Q];
+      P[Q] = *reinterpret_cast<const vecf*>(src + min(i + PF, last_in) * pitch);
       ramp_levels<T, 1>(i, rlo, rhi, upd);
       __builtin_amdgcn_sched_barrier(0);
       ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -231,10 +239,10 @@ struct TbStream {
 #pragma unroll
     for (int s = 0; s < K; ++s)
 #pragma unroll
-      for (int j = 0; j < RING; ++j) R[s][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = 0; j < RING; ++j) R[s][j] = vecf(0.f);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      P[j] = *reinterpret_cast<const float4*>(src + min(first_in + j, last_in) * pitch);
+      P[j] = *reinterpret_cast<const vecf*>(src + min(first_in + j, last_in) * pitch);
     if constexpr (LAG == 4) {
       // As LAG 3, with the main loop unrolled by 6 for the 6-row prefetch ring.
       ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -292,6 +300,8 @@ struct TbStream {
 // path and the ramp otherwise inflate the allocation for every wave).
 template <int K, int LAG>
 constexpr int tb_waves_per_simd() {
+  // float2 lanes: half the ring registers.
+  if (V == 2) return K <= 4 ? 8 : K <= 6 ? 6 : 5;
   if (LAG == 2) return K <= 4 ? 4 : 2;
   if (LAG == 4) return K <= 2 ? 6 : K <= 4 ? 4 : K <= 6 ? 3 : K <= 8 ? 3 : 2;
   return K <= 2 ? 6 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 8 ? 3 : 2;
@@ -299,8 +309,8 @@ constexpr int tb_waves_per_simd() {
 
 template <int K, int LAG>
 __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
-  constexpr int KK = (K + 3) & ~3;
-  constexpr int W = 256 - 2 * KK;
+  constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
+  constexpr int W = 64 * V - 2 * KK;
   const int lane = threadIdx.x & 63;
   int blk = blockIdx.x;
   if (a.flags & tbdetail::kTbXcdGroups) {
@@ -318,7 +328,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   const int strip = w % bx.nstrips, chunk = w / bx.nstrips;
   const int64_t cbase = bx.c0 + int64_t(strip) * W;
   const int64_t cend = min(cbase + W, bx.c1);
-  const int64_t col = cbase - KK + 4 * lane;
+  const int64_t col = cbase - KK + V * lane;
   const bool store_lane = col >= cbase && col < cend;
   const int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
   const int64_t re = min(rb + bx.chunk_len, bx.r1);
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
 
   // Wave-uniform fast path: every row and column the wave touches is a
   // global interior cell, so no Dirichlet masking is needed.
-  const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
+  const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 64 * V - 1;
   const int64_t gx_lo = g.gx0 + rb - K, gx_hi = g.gx0 + re + K - 1;
   // Updatable local rows (global 1..nx-2), clamped into int32.
   int rlo = int(max<int64_t>(1 - g.gx0, -(int64_t(1) << 30)));
@@ -354,7 +364,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   int mode = kModeGeneric;
   if (rows_in && !left && !right) mode = 0;
   else if (rows_in && left && !right && g.gy0 == 0) mode = 1;
-  else if (rows_in && right && !left) mode = 2 + int((g.ny - 1 - g.gy0) & 3);
+  else if (rows_in && right && !left) mode = 2 + int((g.ny - 1 - g.gy0) & (V - 1));
   const int64_t gy = g.gy0 + col;
   auto go = [&](auto mode_c) {
     constexpr int MD = decltype(mode_c)::value;
@@ -362,17 +372,15 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     upd.cx = g.cx;
     upd.cy = g.cy;
     if constexpr (MD == kModeGeneric) {
-      upd.cm0 = in_interior(gy, g.ny);
-      upd.cm1 = in_interior(gy + 1, g.ny);
-      upd.cm2 = in_interior(gy + 2, g.ny);
-      upd.cm3 = in_interior(gy + 3, g.ny);
+#pragma unroll
+      for (int j = 0; j < V; ++j) upd.cm[j] = in_interior(gy + j, g.ny);
     } else if constexpr (MD == 1) {
-      upd.cm0 = gy == 0;  // element 0 of this lane is global column 0
+      upd.cm[0] = gy == 0;  // element 0 of this lane is global column 0
     } else if constexpr (MD >= 2) {
-      upd.cm0 = gy <= g.ny - 1 && g.ny - 1 < gy + 4;  // this lane holds column ny-1
+      upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
     TbStream<K, LAG, MD> st;
-    st.rc = int(min<int64_t>(cend - col, 4));
+    st.rc = int(min<int64_t>(cend - col, V));
     st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
     m = st.m;
   };
@@ -381,8 +389,12 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     case 1: go(std::integral_constant<int, 1>{}); break;
     case 2: go(std::integral_constant<int, 2>{}); break;
     case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 4:
+      if constexpr (V > 2) go(std::integral_constant<int, 4>{});
+      break;
+    case 5:
+      if constexpr (V > 2) go(std::integral_constant<int, 5>{});
+      break;
     default: go(std::integral_constant<int, kModeGeneric>{}); break;
   }
   if (want_resid) wave_max_atomic(m, a.resid);

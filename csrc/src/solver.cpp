@@ -94,8 +94,13 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   L_ = Layout::make(blk_.lx, blk_.ly, H_);
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
   timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
-  alloc();
-  init_fields();
+  try {
+    alloc();
+    init_fields();
+  } catch (...) {
+    free_all();  // the destructor does not run for a throwing constructor
+    throw;
+  }
 }
 
 Solver::~Solver() { free_all(); }
@@ -121,8 +126,6 @@ void Solver::alloc() {
     }
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreate(&ev_t0_));
-    HIP_CHECK(hipEventCreate(&ev_t1_));
     HIP_CHECK(hipMalloc(&d_resid_, 256));
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
@@ -167,7 +170,7 @@ void Solver::free_all() {
     if (h_resid_) (void)hipHostFree(h_resid_);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_checksum_) (void)hipFree(d_checksum_);
-    for (auto e : {ev_ready_, ev_halo_, ev_t0_, ev_t1_})
+    for (auto e : {ev_ready_, ev_halo_})
       if (e) (void)hipEventDestroy(e);
     for (auto e : event_pool_) (void)hipEventDestroy(e);
     event_pool_.clear();
@@ -179,6 +182,12 @@ void Solver::free_all() {
   }
   for (auto& b : base_) b = nullptr;
   for (auto& b : ew_) b = nullptr;
+  for (int i = 0; i < 4; ++i) stage_send_[i] = stage_recv_[i] = nullptr;
+  d_resid_ = nullptr;
+  h_resid_ = nullptr;
+  d_scratch_ = d_checksum_ = nullptr;
+  ev_ready_ = ev_halo_ = nullptr;
+  s_comp_ = s_comm_ = nullptr;
 }
 
 void Solver::init_fields() {

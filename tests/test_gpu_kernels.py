@@ -50,8 +50,9 @@ def test_naive_step_vs_torch(gpu):
 
 
 # 0/3 packed ring-3 (+ramp), 4/7 scalar; +16 XCD-grouped blocks, +32 odd
-# chunks streamed bottom-up (mirrored rows, incl. the plate's top/bottom rows).
-@pytest.mark.parametrize("variant", [0, 3, 4, 7, 23, 39, 55])
+# chunks streamed bottom-up (mirrored rows, incl. the plate's top/bottom rows);
+# +64 float2 lanes (128-column strips).
+@pytest.mark.parametrize("variant", [0, 3, 4, 7, 23, 39, 55, 71, 87, 119])
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     lx, ly = 203, 517  # odd sizes: partial strips and chunks
@@ -63,7 +64,7 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant", [7, 55])
+@pytest.mark.parametrize("variant", [7, 55, 87])
 @pytest.mark.parametrize("waves", [64, 4096])
 def test_tb_chunking_invariance(gpu, waves, variant):
     lx, ly, k = 300, 1000, 8
