@@ -120,7 +120,9 @@ __device__ constexpr int modn(int v) {
   return ((v % N) + N) % N;
 }
 
-template <int K, int LAG, int MODE>
+// RES: this launch computes the fused residual (check passes only); the
+// other passes get an instantiation without the |delta| max per element.
+template <int K, int LAG, int MODE, bool RES>
 struct TbStream {
   static constexpr bool ROWCHK = MODE == kModeGeneric;
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
@@ -136,10 +138,10 @@ struct TbStream {
 
   __device__ __forceinline__ void emit(const vecf& out, const vecf& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
-                                       int64_t re, bool store_lane, bool want_resid) {
+                                       int64_t re, bool store_lane) {
     if (ro >= rb && ro < re && store_lane) {
       *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
-      if (want_resid) {
+      if constexpr (RES) {
         // Columns past the box end (the last lane's spill into padding or
         // stale ghost columns) are written but not part of the residual.
 #pragma unroll
@@ -153,8 +155,7 @@ struct TbStream {
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int rlo, int rhi,
-                                       bool store_lane, const RowUpdate<MODE>& upd,
-                                       bool want_resid) {
+                                       bool store_lane, const RowUpdate<MODE>& upd) {
     if constexpr (LAG == 0) {
       // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
       // s holds rows i-s-2 (slot (U-s)&1) and i-s-1 (slot (U-s-1)&1).
@@ -171,7 +172,7 @@ struct TbStream {
         const int64_t row = i - s - 1;  // row of level s+1 computed now
         const bool ok = !ROWCHK || row_in(row, rlo, rhi);
         const vecf cn = upd(R[s][sa], R[s][sb], c, ok);
-        if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane, want_resid);
+        if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane);
         R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
         c = cn;
       }
@@ -197,7 +198,7 @@ struct TbStream {
       const vecf& b = R[K - 1][modn<RING>(U - rK)];
       const vecf out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
-      emit(out, b, ro, dst, pitch, rb, re, store_lane, want_resid);
+      emit(out, b, ro, dst, pitch, rb, re, store_lane);
     }
   }
 
@@ -230,8 +231,7 @@ struct TbStream {
 
   __device__ __forceinline__ void run(const float* __restrict__ src, float* __restrict__ dst,
                                       int64_t pitch, int64_t rb, int64_t re, int rlo, int rhi,
-                                      bool store_lane, const RowUpdate<MODE>& upd,
-                                      bool want_resid) {
+                                      bool store_lane, const RowUpdate<MODE>& upd) {
     // src/dst are offset to this lane's column; rows are local rows.
     const int64_t first_in = rb - K, last_in = re + K - 1;
     // The last output row (re-1) leaves the pipeline at iteration re-1+SKEW*K.
@@ -250,17 +250,17 @@ struct TbStream {
       for (int64_t t = T0; t < T; t += 6) {
         const int64_t i = first_in + t;
         body<(T0 + 0) % 3, (T0 + 0) % 6>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi,
-                                         store_lane, upd, want_resid);
+                                         store_lane, upd);
         body<(T0 + 1) % 3, (T0 + 1) % 6>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd, want_resid);
+                                         rhi, store_lane, upd);
         body<(T0 + 2) % 3, (T0 + 2) % 6>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd, want_resid);
+                                         rhi, store_lane, upd);
         body<(T0 + 3) % 3, (T0 + 3) % 6>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd, want_resid);
+                                         rhi, store_lane, upd);
         body<(T0 + 4) % 3, (T0 + 4) % 6>(i + 4, t + 4, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd, want_resid);
+                                         rhi, store_lane, upd);
         body<(T0 + 5) % 3, (T0 + 5) % 6>(i + 5, t + 5, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd, want_resid);
+                                         rhi, store_lane, upd);
       }
       return;
     }
@@ -274,24 +274,22 @@ struct TbStream {
       constexpr int U0 = (2 * K) % 3;
       for (int64_t t = 2 * K; t < T; t += 3) {
         const int64_t i = first_in + t;
-        body<U0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
+        body<U0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
         body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
-                           upd, want_resid);
+                           upd);
         body<(U0 + 2) % 3>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
-                           upd, want_resid);
+                           upd);
       }
       return;
     }
     for (int64_t t = 0; t < T; t += RING) {
       const int64_t i = first_in + t;
-      body<0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
-      body<1>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd, want_resid);
+      body<0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
+      body<1>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
       if constexpr (RING >= 3)
-        body<2>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
-                want_resid);
+        body<2>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
       if constexpr (RING == 4)
-        body<3>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
-                want_resid);
+        body<3>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
     }
   }
 };
@@ -366,7 +364,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   else if (rows_in && left && !right && g.gy0 == 0) mode = 1;
   else if (rows_in && right && !left) mode = 2 + int((g.ny - 1 - g.gy0) & (V - 1));
   const int64_t gy = g.gy0 + col;
-  auto go = [&](auto mode_c) {
+  auto go2 = [&](auto mode_c, auto res_c) {
     constexpr int MD = decltype(mode_c)::value;
     RowUpdate<MD> upd;
     upd.cx = g.cx;
@@ -379,10 +377,14 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     } else if constexpr (MD >= 2) {
       upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
-    TbStream<K, LAG, MD> st;
+    TbStream<K, LAG, MD, decltype(res_c)::value> st;
     st.rc = int(min<int64_t>(cend - col, V));
-    st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd, want_resid);
+    st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
     m = st.m;
+  };
+  auto go = [&](auto mode_c) {
+    if (want_resid) go2(mode_c, std::true_type{});
+    else go2(mode_c, std::false_type{});
   };
   switch (mode) {
     case 0: go(std::integral_constant<int, 0>{}); break;
