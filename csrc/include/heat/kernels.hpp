@@ -32,7 +32,8 @@ struct StencilGeom {
 };
 
 // Depths the temporally blocked kernel is instantiated for.
-constexpr int kTbMaxDepth = 8;  // deeper lost every sweep (register bound)
+constexpr int kTbMaxDepth = 8;    // 1..8: every build
+constexpr int kTbDeepDepth = 12;  // + 12: scalar ring-3+ramp build (variant bits 4|3)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.
 // Output columns per TB strip (64 lanes x lane_cols, minus the overlap) and
@@ -76,6 +77,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 int tb_default_variant();
 int tb_variant_lag(int variant);
+// The variant's build has the kTbDeepDepth instantiation (scalar ring-3+ramp).
+bool tb_variant_deep(int variant);
 // Whole rounds of resident waves per launch (HEAT_TB_ROUNDS; 0 = unset: the
 // planner picks waves per SIMD from the work, tb_auto_waves_per_simd).
 int tb_default_rounds();

@@ -75,6 +75,8 @@ class Solver {
   int halo() const { return H_; }
   Schedule schedule() const { return sched_; }
   int tb_depth() const { return T_; }
+  // Default TB depth when neither Params nor HEAT_TB_DEPTH sets one.
+  int auto_tb_depth() const;
   bool on_gpu() const { return P_.backend == Backend::Hip; }
   // The temporally blocked kernel runs the passes (else k single-step launches).
   bool tb_kernel() const {

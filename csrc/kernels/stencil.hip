@@ -158,7 +158,9 @@ int grid_1d(int64_t n) { return int(std::min<int64_t>(ceil_div(n, 256), 256 * 16
 }  // namespace
 
 bool tb_depth_supported(int k) {
-  return k >= 1 && k <= kTbMaxDepth;
+  // 1..8 in every build; 12 in the scalar ring-3+ramp build only
+  // (tb_scalar.hip, HEAT_TB_DEEP).
+  return (k >= 1 && k <= kTbMaxDepth) || k == kTbDeepDepth;
 }
 
 int tb_strip_width(int k, int lane_cols) {
@@ -174,6 +176,10 @@ int tb_variant_lag(int variant) {
     case 3: return 3;
     default: return 1;
   }
+}
+
+bool tb_variant_deep(int variant) {
+  return (variant & 4) && !(variant & 64) && tb_variant_lag(variant) == 3;
 }
 
 int tb_default_rounds() {
@@ -357,7 +363,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   const bool ok = (variant & 64)  ? tbn::launch(args, depth, lag, st)
                   : (variant & 4) ? tbs::launch(args, depth, lag, st)
                                   : tbp::launch(args, depth, lag, st);
-  HEAT_CHECK(ok, "unsupported TB depth %d", depth);
+  HEAT_CHECK(ok, "TB depth %d is not instantiated for variant %d (depth %d: scalar ring-3+ramp only)",
+             depth, variant, kTbDeepDepth);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -5,4 +5,7 @@
 
 #define HEAT_TB_NS tbs
 #define HEAT_TB_PACKED 0
+// Depth 12 (ring-3 + ramp only): 2/3 the HBM bytes per update of depth 8,
+// at 2 waves/SIMD; see tb_depth_supported().
+#define HEAT_TB_DEEP 1
 #include "tb_stream.inl"

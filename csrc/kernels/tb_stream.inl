@@ -402,6 +402,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   if (want_resid) wave_max_atomic(m, a.resid);
 }
 
+#ifndef HEAT_TB_EXPERIMENT  // experiments instantiate tb_kernel<K, LAG> themselves
 template <int K, int LAG>
 void launch_k(const TbArgs& args, hipStream_t st) {
   const int blocks = int((args.total_waves + 3) / 4);
@@ -427,6 +428,9 @@ int occ_k() {
 
 // Resident 256-thread blocks per CU of the (depth, lag) instantiation.
 int occupancy(int depth, int lag) {
+#if HEAT_TB_DEEP
+  if (lag == 3 && depth == 12) return occ_k<12, 3>();
+#endif
   if (lag == 3) {
   switch (depth) {
     case 1: return occ_k<1, 3>();
@@ -461,6 +465,16 @@ int occupancy(int depth, int lag) {
 // (LAG 2) and 2-slot (LAG 0) forms lost every sweep (profiles/tb_sweep_*.json)
 // and only cost build time.
 bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
+#if HEAT_TB_DEEP
+  // K = 12: 2 waves/SIMD (256 VGPRs; the main loop is spill-free, the
+  // unrolled ramp spills a little); 2/3 the HBM bytes per update of K = 8.
+  // K = 10 measured between 8 and 12, K = 16 spills in the main loop
+  // (profiles/tb_depth_sweep_r1.md).
+  if (lag == 3 && depth == 12) {
+    launch_k<12, 3>(args, st);
+    return true;
+  }
+#endif
   if (lag == 3) {
   switch (depth) {
     case 1: launch_k<1, 3>(args, st); return true;
@@ -487,4 +501,5 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
   }
 }
 
+#endif  // HEAT_TB_EXPERIMENT
 }  // namespace heat::gpu::HEAT_TB_NS

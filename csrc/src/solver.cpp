@@ -52,7 +52,8 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
     if (!tb_kernel()) {
       T_ = P_.tb_depth > 0 ? P_.tb_depth : 1;
     } else {
-      T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 8);
+      T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 0);
+      if (T_ == 0) T_ = auto_tb_depth();
       HEAT_CHECK(gpu::tb_depth_supported(T_), "TB depth %d not supported", T_);
     }
   } else {
@@ -210,9 +211,39 @@ int64_t Solver::configured_steps(int64_t steps) const {
   return P_.compat == Compat::Mpi ? steps + 1 : steps;
 }
 
+int Solver::auto_tb_depth() const {
+  // Depth 12 (2/3 the HBM bytes per update of 8, at 2 waves/SIMD) wins on
+  // tall blocks and loses a little below ~3K rows, where the longer ramp of
+  // the shorter chunks costs more than the bytes it saves
+  // (profiles/tb_depth_sweep_r1.md).  Decided from the smallest block of any
+  // rank, so every rank picks the same depth.
+  if (!gpu::tb_variant_deep(gpu::tb_default_variant())) return 8;
+  int64_t min_lx = INT64_MAX;
+  for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
+  return min_lx >= 3072 ? gpu::kTbDeepDepth : 8;
+}
+
 std::vector<int> Solver::pass_depths(int64_t n) const {
   std::vector<int> d;
   const bool tb = tb_kernel();
+  if (tb && T_ > gpu::kTbMaxDepth) {
+    // Deep passes, then the remainder in near-equal passes of at most
+    // kTbMaxDepth.  A short remainder (1000 = 83 x 12 + 4, 50 = 4 x 12 + 2)
+    // is folded together with the last deep pass: the pass count stays the
+    // same and no pass moves the whole field for only a few steps.
+    const int64_t q = n / T_;
+    int total = int(n % T_);
+    d.assign(size_t(q), T_);
+    if (total > 0) {
+      if (total < gpu::kTbMaxDepth && q >= 1) {
+        d.pop_back();
+        total += T_;
+      }
+      const int parts = (total + gpu::kTbMaxDepth - 1) / gpu::kTbMaxDepth;
+      for (int i = 0; i < parts; ++i) d.push_back(total / parts + (i < total % parts ? 1 : 0));
+    }
+    return d;
+  }
   while (n > 0) {
     int k = int(std::min<int64_t>(T_, n));
     if (tb)

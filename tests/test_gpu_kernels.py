@@ -64,6 +64,19 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
+@pytest.mark.parametrize("variant", [7, 23])
+@pytest.mark.parametrize("depth", [12])
+def test_tb_deep_bitwise_vs_cpu_oracle(gpu, depth, variant):
+    # Depth 12 exists in the scalar ring-3+ramp build only.
+    lx, ly = 203, 517
+    g, a, b = _fields(lx, ly, depth, gpu)
+    ops.tb_step(a, b, g, depth, variant=variant)
+    torch.cuda.synchronize()
+    ref = _cpu_steps(g, lx, ly, depth, depth)
+    got = b.owned().cpu()
+    assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
+
+
 @pytest.mark.parametrize("variant", [7, 55, 87])
 @pytest.mark.parametrize("waves", [64, 4096])
 def test_tb_chunking_invariance(gpu, waves, variant):

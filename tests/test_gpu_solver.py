@@ -27,6 +27,31 @@ def test_gpu_equals_cpu(gpu, kernel, depth, graph):
     assert np.array_equal(g, c), np.abs(g - c).max()
 
 
+@pytest.mark.parametrize("steps", [45, 50, 1000])
+def test_gpu_depth12_passes(gpu, steps):
+    # Depth 12 with the remainder in near-equal passes of <= 8
+    # (45 -> 12,12,12,5,4; 50 -> 12,12,12,7,7; 1000 -> 82 x 12,8,8).
+    cfg = HeatConfig(nx=150, ny=333, steps=steps, init="random", seed=4, backend="hip",
+                     tb_depth=12)
+    g, r = _run(cfg)
+    c, _ = _run(cfg.replace(backend="cpu", tb_depth=1))
+    assert r.steps_done == steps
+    assert np.array_equal(g, c), np.abs(g - c).max()
+
+
+def test_gpu_auto_depth_tall_block(gpu):
+    # Blocks of >= 3072 rows get depth 12 by default, shorter ones depth 8.
+    tall = HeatConfig(nx=3100, ny=70, steps=30, init="random", seed=6, backend="hip")
+    with HeatSolver(tall) as s:
+        assert s.info.tb_depth == 12
+        s.run()
+        g = s.gather()
+    c, _ = _run(tall.replace(backend="cpu"))
+    assert np.array_equal(g, c)
+    with HeatSolver(tall.replace(nx=3000)) as s:
+        assert s.info.tb_depth == 8
+
+
 def test_reference_init_grid(gpu):
     cfg = HeatConfig(nx=500, ny=500, steps=100, init="ref-wrap", backend="hip")
     g, _ = _run(cfg)
