@@ -43,11 +43,16 @@ using heat::gpu::tbdetail::TbBox;
 using heat::gpu::tbdetail::in_interior;
 using heat::gpu::tbdetail::wave_max_atomic;
 
+// Lane 0 (from_left) / lane 63 (from_right) has no source lane and reads 0
+// (bound_ctrl); those lanes lie in the strip overlap, so the value is
+// don't-care.  bound_ctrl lets the compiler fold both shifts into the
+// consuming v_add_f32_dpp; with old = 0 and bound_ctrl off it only folded
+// wave_shr and materialised wave_shl as v_mov 0 + v_mov_b32_dpp + v_add.
 __device__ __forceinline__ float dpp_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // Dirichlet handling modes (wave-uniform, chosen per wave in tb_kernel).
@@ -92,7 +97,11 @@ struct RowUpdate {
     for (int j = 0; j < V; ++j) {
       const float w = j == 0 ? dpp_from_left(b[V - 1]) : b[j - 1];
       const float e = j == V - 1 ? dpp_from_right(b[0]) : b[j + 1];
-      r[j] = stencil(b[j], a[j], c[j], w, e, cx, cy);
+      // stencil() sums e + w; for the last element pass them swapped (fp add
+      // commutes, bitwise identical) so the DPP value is the operand the
+      // compiler folds into v_add_f32_dpp, as it does for the first element.
+      r[j] = j == V - 1 ? stencil(b[j], a[j], c[j], e, w, cx, cy)
+                        : stencil(b[j], a[j], c[j], w, e, cx, cy);
     }
 #endif
     if constexpr (MODE == kModeGeneric) {
