@@ -136,6 +136,9 @@ int heat_op_lds_step(const float* src, float* dst, int64_t pitch, int64_t gx0, i
 int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                       int64_t nx, int64_t ny, float cx, float cy, int64_t r0, int64_t r1,
                       int64_t c0, int64_t c1, unsigned* resid, void* stream);
+// Diagnostics: per-wave start/end clock stamps of subsequent TB launches
+// (4 u64 per wave: start, end at 100 MHz, block, strip<<32|chunk); null = off.
+int heat_op_tb_stamps(void* buf, int64_t waves);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,

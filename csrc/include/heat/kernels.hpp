@@ -33,6 +33,12 @@ struct StencilGeom {
 
 // Depths the temporally blocked kernel is instantiated for.
 constexpr int kTbMaxDepth = 8;    // 1..8: every build
+// Rows of the older : younger wave of a chunk pair at two waves per SIMD
+// (kTbAgePairs; HEAT_TB_AGE_RATIO sets it, <= 1 = off).  Off by default: it
+// evens the two waves' finish times (busy fraction 0.77 -> 0.81) but not the
+// launch span, which the SIMD's combined issue rate sets
+// (profiles/tb_wave_timeline_r1.md).
+constexpr double kTbAgeRatio = 1.0;
 constexpr int kTbDeepDepth = 12;  // + 12: scalar ring-3+ramp build (variant bits 4|3)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.
@@ -76,6 +82,10 @@ void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& bo
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 int tb_default_variant();
+// Diagnostics: while set, every tb_step launch writes 4 u64 per wave into buf
+// ({start, end} s_memrealtime ticks (100 MHz), block, strip<<32 | chunk);
+// waves = buffer capacity in waves.  nullptr switches it off.
+void tb_set_stamps(unsigned long long* buf, int64_t waves);
 int tb_variant_lag(int variant);
 // The variant's build has the kTbDeepDepth instantiation (scalar ring-3+ramp).
 bool tb_variant_deep(int variant);

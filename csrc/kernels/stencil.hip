@@ -262,6 +262,16 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
   HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+unsigned long long* g_tb_stamps = nullptr;
+int64_t g_tb_stamp_waves = 0;
+}  // namespace
+
+void tb_set_stamps(unsigned long long* buf, int64_t waves) {
+  g_tb_stamps = buf;
+  g_tb_stamp_waves = waves;
+}
+
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
@@ -272,6 +282,13 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   int64_t total_strip_rows = 0;
   for (int b = 0; b < nbox; ++b)
     if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
+  // Age pairs (kTbAgePairs) for launches of exactly two waves per SIMD
+  // chosen by the planner; HEAT_TB_AGE_RATIO = older:younger rows (<= 1: off).
+  static const double age_ratio = [] {
+    const char* e = std::getenv("HEAT_TB_AGE_RATIO");
+    return e && *e ? std::atof(e) : kTbAgeRatio;
+  }();
+  bool pairs = (variant & 256) != 0;  // bit 256: force age pairs (tests)
   if (waves_target <= 0) {
     // Whole rounds of the resident wave capacity (a partial last round leaves
     // SIMDs idle for the tail of the launch); by default with the number of
@@ -282,8 +299,10 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       waves_target = rounds * resident;
     } else {
       const int simds = tb_simd_count();
-      waves_target = simds * tb_auto_waves_per_simd(depth, total_strip_rows / simds,
-                                                    std::max(1, resident / simds));
+      const int per_simd = tb_auto_waves_per_simd(depth, total_strip_rows / simds,
+                                                  std::max(1, resident / simds));
+      waves_target = simds * per_simd;
+      pairs = pairs || (per_simd == 2 && age_ratio > 1.0 && !(variant & 64));
     }
   }
   TbArgs args{};
@@ -292,7 +311,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.resid = resid;
   args.g = g;
   args.flags = ((variant & 16) ? tbdetail::kTbXcdGroups : 0) |
-               ((variant & 32) ? tbdetail::kTbAltDirection : 0);
+               ((variant & 32) ? tbdetail::kTbAltDirection : 0) |
+               ((variant & 1024) ? tbdetail::kTbDiagNoStore : 0);
   // Split rows into chunks so the whole launch has about waves_target waves,
   // but never shorter than 4*depth rows (keeps the redundant 2*depth-row
   // halo reads below ~50 %).
@@ -324,8 +344,15 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       t.nstrips = int(ceil_div(B.cols(), W));
       t.chunk_len = int(std::min<int64_t>(clen, B.rows()));
       t.nchunks = int(ceil_div(B.rows(), t.chunk_len));
+      t.age_delta = 0;
+      if (pairs) {
+        // Units are chunk pairs (2 * chunk_len rows), one wave of each half.
+        t.chunk_len = int(std::max<int64_t>(1, ceil_div(std::min<int64_t>(2 * clen, B.rows()), 2)));
+        t.nchunks = int(ceil_div(B.rows(), 2 * int64_t(t.chunk_len)));
+        t.age_delta = int(double(t.chunk_len) * (age_ratio - 1.0) / (age_ratio + 1.0));
+      }
       t.wave_begin = waves;
-      waves += t.nstrips * t.nchunks;
+      waves += t.nstrips * t.nchunks * (pairs ? 2 : 1);
     };
     for (int b = 0; b < nbox; ++b) {
       const Box& B = boxes[b];
@@ -360,6 +387,17 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   if (n == 0) return;
   args.nbox = n;
   args.total_waves = waves;
+  if (pairs) {
+    // wave_begin / total_waves count pairs (waves of one half).
+    for (int b = 0; b < n; ++b) args.box[b].wave_begin /= 2;
+    args.total_waves = waves / 2;
+    args.flags |= tbdetail::kTbAgePairs;
+  }
+  if (g_tb_stamps) {
+    HEAT_CHECK(int64_t(waves) <= g_tb_stamp_waves, "stamp buffer holds %lld waves, launch has %d",
+               (long long)g_tb_stamp_waves, waves);
+    args.stamps = g_tb_stamps;
+  }
   const bool ok = (variant & 64)  ? tbn::launch(args, depth, lag, st)
                   : (variant & 4) ? tbs::launch(args, depth, lag, st)
                                   : tbp::launch(args, depth, lag, st);

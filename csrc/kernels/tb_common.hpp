@@ -13,6 +13,7 @@ namespace heat::gpu::tbdetail {
 struct TbBox {
   int64_t r0, r1, c0, c1;
   int nstrips, nchunks, chunk_len, wave_begin;
+  int age_delta;  // kTbAgePairs: extra rows of the older wave of a chunk pair
 };
 
 constexpr int kMaxBoxes = 16;
@@ -24,6 +25,11 @@ struct TbArgs {
   StencilGeom g;
   int nbox, total_waves;
   int flags;  // kTbXcdGroups | kTbAltDirection
+  // Diagnostics (null in production): per wave {start, end} of the global
+  // 100 MHz s_memrealtime clock, block<<40 | XCC_ID<<32 | HW_ID and
+  // strip<<32 | chunk, 4 u64
+  // per wave index; see tb_set_stamps().
+  unsigned long long* stamps;
   TbBox box[kMaxBoxes];
 };
 
@@ -36,6 +42,15 @@ struct TbArgs {
 //                    time (both at the start or both at the end).
 constexpr int kTbXcdGroups = 1;
 constexpr int kTbAltDirection = 2;
+//   kTbAgePairs      two waves per SIMD split each pair of adjacent chunks
+//                    unevenly, the older (first-dispatched) wave taking more
+//                    rows: with equal chunks the older wave finishes at ~60 %
+//                    of the launch and the younger one runs the rest alone
+//                    (tools/wave_timeline.py, profiles/tb_age_pairs_r1.md).
+constexpr int kTbAgePairs = 4;
+//   kTbDiagNoStore   diagnostics: skip the output stores (wrong results; a
+//                    timing probe of the store traffic; variant bit 1024).
+constexpr int kTbDiagNoStore = 8;
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
 

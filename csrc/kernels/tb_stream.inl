@@ -55,6 +55,17 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
+// A wave-uniform value moved into a VGPR.  A VALU instruction with an SGPR
+// operand issues at half rate on gfx950 (tools/probes/valu_rate.hip:
+// v_fmac_f32 v,s,v ~4.4 cycles vs ~2.6 for v,v,v at 4 waves/SIMD), and the
+// update's two coefficient FMAs would otherwise read cx/cy from SGPRs.  The
+// asm result is opaque, so the compiler cannot fold it back into an SGPR.
+__device__ __forceinline__ float to_vgpr(float x) {
+  float r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
 // Dirichlet handling modes (wave-uniform, chosen per wave in tb_kernel).
 // Cells outside the plate are don't-care (their values only ever flow
 // further out), so only the boundary ring itself must be kept:
@@ -144,12 +155,13 @@ struct TbStream {
   vecf P[PF];       // prefetch ring (input row i + PF)
   unsigned m = 0;
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
+  bool nostore = false;  // diagnostics only (kTbDiagNoStore): timing without the stores
 
   __device__ __forceinline__ void emit(const vecf& out, const vecf& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
                                        int64_t re, bool store_lane) {
     if (ro >= rb && ro < re && store_lane) {
-      *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
+      if (!nostore) *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
       if constexpr (RES) {
         // Columns past the box end (the last lane's spill into padding or
         // stale ghost columns) are written but not part of the residual.
@@ -319,13 +331,25 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
   constexpr int W = 64 * V - 2 * KK;
   const int lane = threadIdx.x & 63;
-  int blk = blockIdx.x;
+  // Age pairs (kTbAgePairs): the grid is two halves of one block per CU
+  // each; a CU runs block i of the first half (dispatched first: the OLDER
+  // wave on each SIMD, which the SIMD's issue arbitration favours) next to
+  // block i of the second half.  Wave i of both halves takes the same pair
+  // of vertically adjacent chunks, the older one the longer share.
+  const bool pairs = a.flags & tbdetail::kTbAgePairs;
+  int nb = gridDim.x, blk = blockIdx.x, age = 0;
+  if (pairs) {
+    nb >>= 1;
+    age = blk >= nb;
+    blk -= age * nb;
+  }
   if (a.flags & tbdetail::kTbXcdGroups) {
-    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = blk & 7, j = blk >> 3;
+    const int q = nb >> 3, r = nb & 7, x = blk & 7, j = blk >> 3;
     blk = x * q + min(x, r) + j;
   }
   const int wave = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave >= a.total_waves) return;
+  const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   int bi = 0;
 #pragma unroll
   for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
@@ -337,8 +361,18 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   const int64_t cend = min(cbase + W, bx.c1);
   const int64_t col = cbase - KK + V * lane;
   const bool store_lane = col >= cbase && col < cend;
-  const int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
-  const int64_t re = min(rb + bx.chunk_len, bx.r1);
+  int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
+  int64_t re = min(rb + bx.chunk_len, bx.r1);
+  if (pairs) {
+    // Box chunks are pairs of 2 * chunk_len rows; the older wave takes
+    // chunk_len + delta of them.
+    const int64_t p0 = bx.r0 + int64_t(chunk) * 2 * bx.chunk_len;
+    const int64_t p1 = min(p0 + 2 * int64_t(bx.chunk_len), bx.r1);
+    const int64_t split = min(p0 + bx.chunk_len + bx.age_delta, p1);
+    rb = age ? split : p0;
+    re = age ? p1 : split;
+    if (rb >= re) return;
+  }
 
   const StencilGeom& g = a.g;
   const float* src = a.src + col;
@@ -376,8 +410,8 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
   auto go2 = [&](auto mode_c, auto res_c) {
     constexpr int MD = decltype(mode_c)::value;
     RowUpdate<MD> upd;
-    upd.cx = g.cx;
-    upd.cy = g.cy;
+    upd.cx = to_vgpr(g.cx);
+    upd.cy = to_vgpr(g.cy);
     if constexpr (MD == kModeGeneric) {
 #pragma unroll
       for (int j = 0; j < V; ++j) upd.cm[j] = in_interior(gy + j, g.ny);
@@ -388,6 +422,7 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     }
     TbStream<K, LAG, MD, decltype(res_c)::value> st;
     st.rc = int(min<int64_t>(cend - col, V));
+    st.nostore = a.flags & tbdetail::kTbDiagNoStore;
     st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
     m = st.m;
   };
@@ -409,12 +444,23 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     default: go(std::integral_constant<int, kModeGeneric>{}); break;
   }
   if (want_resid) wave_max_atomic(m, a.resid);
+  if (a.stamps && lane == 0) {
+    unsigned long long* st = a.stamps + 4 * (int64_t(wave) + int64_t(age) * a.total_waves);
+    st[0] = t_start;
+    st[1] = __builtin_amdgcn_s_memrealtime();
+    // HW_ID (wave, SIMD, CU, SE ids) and XCC_ID via s_getreg.
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+    st[2] = ((unsigned long long)blockIdx.x << 40) | ((unsigned long long)xcc << 32) | hw;
+    st[3] = ((unsigned long long)strip << 32) | unsigned(chunk);
+  }
 }
 
 #ifndef HEAT_TB_EXPERIMENT  // experiments instantiate tb_kernel<K, LAG> themselves
 template <int K, int LAG>
 void launch_k(const TbArgs& args, hipStream_t st) {
-  const int blocks = int((args.total_waves + 3) / 4);
+  int blocks = int((args.total_waves + 3) / 4);
+  if (args.flags & tbdetail::kTbAgePairs) blocks *= 2;  // two halves, see tb_kernel
   hipLaunchKernelGGL((tb_kernel<K, LAG>), dim3(blocks), dim3(256), 0, st, args);
 }
 

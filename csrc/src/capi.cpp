@@ -400,6 +400,10 @@ int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, in
   });
 }
 
+int heat_op_tb_stamps(void* buf, int64_t waves) {
+  return guard([&] { heat::gpu::tb_set_stamps(static_cast<unsigned long long*>(buf), waves); });
+}
+
 int heat_op_init(float* origin, int64_t lx, int64_t ly, int halo, int64_t gx0, int64_t gy0,
                  int64_t nx, int64_t ny, int mode, uint64_t seed, void* stream) {
   return guard([&] {

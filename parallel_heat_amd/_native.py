@@ -147,6 +147,7 @@ _SIGS = {
     "heat_op_tb_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                 c_float, c_float, POINTER(c_int64), c_int, c_int, c_void_p,
                                 c_void_p, c_int, c_int]),
+    "heat_op_tb_stamps": (c_int, [c_void_p, c_int64]),
     "heat_op_init": (c_int, [c_void_p, c_int64, c_int64, c_int, c_int64, c_int64, c_int64,
                              c_int64, c_int, c_uint64, c_void_p]),
     "heat_op_pack": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_void_p,

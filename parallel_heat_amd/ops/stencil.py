@@ -172,6 +172,18 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
                  ctypes.c_void_p(_stream()), waves_target, variant)
 
 
+def tb_stamps(buf: Optional[torch.Tensor]) -> None:
+    """Diagnostics: record per-wave clock stamps of the following tb_step
+    launches into `buf` (int64 GPU tensor, 4 per wave: start, end in 100 MHz
+    ticks, block, strip << 32 | chunk); None switches recording off."""
+    if buf is None:
+        _native.call("heat_op_tb_stamps", None, 0)
+        return
+    if buf.dtype != torch.int64 or buf.device.type != "cuda":
+        raise ValueError("stamps need an int64 GPU tensor")
+    _native.call("heat_op_tb_stamps", ctypes.c_void_p(buf.data_ptr()), buf.numel() // 4)
+
+
 def pack(f: Field, box: Box, out: torch.Tensor) -> None:
     r0, r1, c0, c1 = box
     if f.device.type == "cpu":

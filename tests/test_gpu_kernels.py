@@ -64,13 +64,29 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant", [7, 23])
-@pytest.mark.parametrize("depth", [12])
+@pytest.mark.parametrize("variant,depth", [(7, 12), (23, 12), (55, 12), (279, 12)])
 def test_tb_deep_bitwise_vs_cpu_oracle(gpu, depth, variant):
-    # Depth 12 exists in the scalar ring-3+ramp build only.
+    # Depth 12 exists in the scalar ring-3+ramp build only (+32 mirrored odd
+    # chunks, +256 age pairs).
     lx, ly = 203, 517
     g, a, b = _fields(lx, ly, depth, gpu)
     ops.tb_step(a, b, g, depth, variant=variant)
+    torch.cuda.synchronize()
+    ref = _cpu_steps(g, lx, ly, depth, depth)
+    got = b.owned().cpu()
+    assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
+
+
+@pytest.mark.parametrize("variant", [263, 279, 311])  # +256: age-paired chunks forced
+@pytest.mark.parametrize("depth", [3, 8, 12])
+@pytest.mark.parametrize("waves", [0, 64, 1000, 4096])
+def test_tb_age_pairs_bitwise(gpu, depth, variant, waves):
+    # Chunk pairs split unevenly between the two waves of a SIMD (older wave
+    # longer), odd sizes so pairs are cut by the box end; the tall block makes
+    # the planner's own two-waves-per-SIMD choice pair chunks too (waves 0).
+    lx, ly = (203, 517) if waves else (2600, 300)
+    g, a, b = _fields(lx, ly, depth, gpu)
+    ops.tb_step(a, b, g, depth, waves_target=waves, variant=variant)
     torch.cuda.synchronize()
     ref = _cpu_steps(g, lx, ly, depth, depth)
     got = b.owned().cpu()

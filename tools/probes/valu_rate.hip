@@ -13,6 +13,10 @@ constexpr int NCH = 16;
 
 template <int KIND>
 __global__ __launch_bounds__(256) void probe(float* out, int iters, float a, float b) {
+  if constexpr (KIND == 11) asm("v_mov_b32 %0, %1" : "=v"(b) : "s"(b));
+  float cf[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) asm("v_mov_b32 %0, %1" : "=v"(cf[q]) : "s"(b));
   float v[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) v[j] = float(threadIdx.x + j);
@@ -27,6 +31,24 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float a, flo
         v[j] = __builtin_fmaf(v[(j + 3) % NCH], v[(j + 1) % NCH], v[j]);
       } else if constexpr (KIND == 3) {  // v_add_f32_dpp (wave_shr:1)
         v[j] = v[j] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[(j + 5) % NCH]), 0x138, 0xf, 0xf, false));
+      } else if constexpr (KIND == 5) {  // v_fmac_f32 v, s, v (one SGPR operand)
+        v[j] = __builtin_fmaf(a, v[(j + 3) % NCH], v[j]);
+      } else if constexpr (KIND == 6) {  // v_fmac_f32 v, -2.0, v (inline constant)
+        v[j] = __builtin_fmaf(-2.0f, v[(j + 3) % NCH], v[j]);
+      } else if constexpr (KIND == 7) {  // v_fma_f32 v, s, v, v (one SGPR, 3 operands)
+        v[j] = __builtin_fmaf(a, v[(j + 3) % NCH], v[(j + 7) % NCH]);
+      } else if constexpr (KIND == 8) {  // v_fmac_f32 with operands 4 and 8 registers apart
+        v[j] = __builtin_fmaf(v[(j + 4) % NCH], v[(j + 8) % NCH], v[j]);
+      } else if constexpr (KIND == 9) {  // v_fmac_f32 with operands 1 and 2 registers apart
+        v[j] = __builtin_fmaf(v[(j + 1) % NCH], v[(j + 2) % NCH], v[j]);
+      } else if constexpr (KIND == 10) {  // v_fma_f32 VOP3, all VGPRs, separate destination
+        v[j] = __builtin_fmaf(v[(j + 1) % NCH], v[(j + 2) % NCH], v[(j + 3) % NCH]);
+      } else if constexpr (KIND == 11) {  // v_fmac_f32 v, v, v with a VGPR coefficient (cx)
+        v[j] = __builtin_fmaf(b, v[(j + 2) % NCH], v[j]);
+      } else if constexpr (KIND == 12) {  // v_fmac_f32 v, 0.1 literal, v
+        v[j] = __builtin_fmaf(0.1f, v[(j + 2) % NCH], v[j]);
+      } else if constexpr (KIND == 13) {  // as 11, 16 chains reading 4 distinct coefficient copies
+        v[j] = __builtin_fmaf(cf[j & 3], v[(j + 2) % NCH], v[j]);
       } else if constexpr (KIND == 4) {  // v_pk_fma_f32 (2 lanes per op)
         typedef float f2 __attribute__((ext_vector_type(2)));
         f2 x = {v[j], v[(j + 8) % NCH]};
@@ -66,9 +88,13 @@ int main() {
   float* out;
   CHECK(hipMalloc(&out, 4096));
   const int iters = 20000;
-  const char* names[] = {"v_fmac_f32 (v,s,s)", "v_add_f32 (v,v)", "v_fma_f32 (v,v,v)", "v_add_f32_dpp", "v_pk_fma_f32"};
-  const int per_body[] = {NCH, NCH, NCH, NCH, NCH / 1};
-  for (int kind = 0; kind < 5; ++kind) {
+  const char* names[] = {"v_fma_f32 (v,v,s,s)", "v_add_f32 (v,v)", "v_fmac_f32 (v,v,v)", "v_add_f32_dpp",
+                         "v_pk_fma_f32", "v_fmac_f32 (v,s,v)", "v_fmac_f32 (v,-2.0,v)", "v_fma_f32 (v,s,v,v)",
+                         "v_fmac_f32 operands +4,+8 regs", "v_fmac_f32 operands +1,+2 regs",
+                         "v_fma_f32 (v,v,v,v) VOP3", "v_fmac_f32 (v, vgpr coef, v)",
+                         "v_fmac_f32 (v, 0.1 literal, v)", "v_fmac_f32 (v, 4 vgpr coef copies, v)"};
+  const int per_body[] = {NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH};
+  for (int kind = 0; kind < 14; ++kind) {
     for (int w : {1, 2, 3, 4}) {
       double ms = 0;
       switch (kind) {
@@ -77,6 +103,15 @@ int main() {
         case 2: ms = run<2>(w, cus, iters, out); break;
         case 3: ms = run<3>(w, cus, iters, out); break;
         case 4: ms = run<4>(w, cus, iters, out); break;
+        case 5: ms = run<5>(w, cus, iters, out); break;
+        case 6: ms = run<6>(w, cus, iters, out); break;
+        case 7: ms = run<7>(w, cus, iters, out); break;
+        case 8: ms = run<8>(w, cus, iters, out); break;
+        case 9: ms = run<9>(w, cus, iters, out); break;
+        case 10: ms = run<10>(w, cus, iters, out); break;
+        case 11: ms = run<11>(w, cus, iters, out); break;
+        case 12: ms = run<12>(w, cus, iters, out); break;
+        case 13: ms = run<13>(w, cus, iters, out); break;
       }
       // instructions per SIMD = waves/SIMD x iters x body
       const double instr = double(w) * iters * per_body[kind];
