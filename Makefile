@@ -29,7 +29,7 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
-$(BUILD)/obj/tb_scalar.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip $(HDRS) $(KHDRS)
 	@mkdir -p $(dir $@)

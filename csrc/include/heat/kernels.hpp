@@ -89,6 +89,9 @@ void tb_set_stamps(unsigned long long* buf, int64_t waves);
 int tb_variant_lag(int variant);
 // The variant's build has the kTbDeepDepth instantiation (scalar ring-3+ramp).
 bool tb_variant_deep(int variant);
+// Bit 2048: each (strip, chunk) runs on a two-wave level-split pipeline
+// (depths 8 and 12; scalar ring-3+ramp variants only).
+bool tb_variant_split(int variant);
 // Whole rounds of resident waves per launch (HEAT_TB_ROUNDS; 0 = unset: the
 // planner picks waves per SIMD from the work, tb_auto_waves_per_simd).
 int tb_default_rounds();

@@ -178,6 +178,11 @@ int tb_variant_lag(int variant) {
   }
 }
 
+bool tb_variant_split(int variant) {
+  // Bit 2048: level-split two-wave pipelines (tb_split.hip; scalar ring-3+ramp).
+  return (variant & 2048) && (variant & 4) && !(variant & 64) && tb_variant_lag(variant) == 3;
+}
+
 bool tb_variant_deep(int variant) {
   return (variant & 4) && !(variant & 64) && tb_variant_lag(variant) == 3;
 }
@@ -228,6 +233,12 @@ int tb_resident_waves(int depth, int variant) {
   int cus = 0;
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int lag = tb_variant_lag(variant);
+  if (tb_variant_split(variant)) {
+    // Work units are two-wave pipelines, two per block.
+    const int w = std::max(1, cus * std::max(1, tbx::occupancy_split(depth)) * 2);
+    cache.emplace(key, w);
+    return w;
+  }
   const int per_cu = (variant & 64)  ? tbn::occupancy(depth, lag)
                      : (variant & 4) ? tbs::occupancy(depth, lag)
                                      : tbp::occupancy(depth, lag);
@@ -312,7 +323,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.g = g;
   args.flags = ((variant & 16) ? tbdetail::kTbXcdGroups : 0) |
                ((variant & 32) ? tbdetail::kTbAltDirection : 0) |
-               ((variant & 1024) ? tbdetail::kTbDiagNoStore : 0);
+               ((variant & 1024) ? tbdetail::kTbDiagNoStore : 0) |
+               ((variant & 4096) ? tbdetail::kTbDiagCachedRows : 0);
   // Split rows into chunks so the whole launch has about waves_target waves,
   // but never shorter than 4*depth rows (keeps the redundant 2*depth-row
   // halo reads below ~50 %).
@@ -393,14 +405,17 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     args.total_waves = waves / 2;
     args.flags |= tbdetail::kTbAgePairs;
   }
+  const bool split = tb_variant_split(variant);
   if (g_tb_stamps) {
-    HEAT_CHECK(int64_t(waves) <= g_tb_stamp_waves, "stamp buffer holds %lld waves, launch has %d",
-               (long long)g_tb_stamp_waves, waves);
+    const int64_t need = int64_t(waves) * (split ? 2 : 1);
+    HEAT_CHECK(need <= g_tb_stamp_waves, "stamp buffer holds %lld waves, launch has %lld",
+               (long long)g_tb_stamp_waves, (long long)need);
     args.stamps = g_tb_stamps;
   }
-  const bool ok = (variant & 64)  ? tbn::launch(args, depth, lag, st)
-                  : (variant & 4) ? tbs::launch(args, depth, lag, st)
-                                  : tbp::launch(args, depth, lag, st);
+  const bool ok = split           ? tbx::launch_split(args, depth, st)
+                  : (variant & 64) ? tbn::launch(args, depth, lag, st)
+                  : (variant & 4)  ? tbs::launch(args, depth, lag, st)
+                                   : tbp::launch(args, depth, lag, st);
   HEAT_CHECK(ok, "TB depth %d is not instantiated for variant %d (depth %d: scalar ring-3+ramp only)",
              depth, variant, kTbDeepDepth);
   HIP_CHECK(hipGetLastError());

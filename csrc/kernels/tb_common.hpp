@@ -17,6 +17,8 @@ struct TbBox {
 };
 
 constexpr int kMaxBoxes = 16;
+// Rows of the LDS ring between the two stages of a level-split pipeline.
+constexpr int kSplitRing = 8;
 
 struct TbArgs {
   const float* src;
@@ -51,6 +53,10 @@ constexpr int kTbAgePairs = 4;
 //   kTbDiagNoStore   diagnostics: skip the output stores (wrong results; a
 //                    timing probe of the store traffic; variant bit 1024).
 constexpr int kTbDiagNoStore = 8;
+//   kTbDiagCachedRows diagnostics: every input row load reads one of the
+//                    chunk's first 4 rows (cache-resident; wrong results, a
+//                    probe of load latency; variant bit 4096).
+constexpr int kTbDiagCachedRows = 16;
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
 
@@ -69,6 +75,10 @@ int occupancy(int depth, int lag);
 namespace heat::gpu::tbs {
 bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);
 int occupancy(int depth, int lag);
+}
+namespace heat::gpu::tbx {  // level-split two-wave pipelines (tb_split.hip)
+bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);
+int occupancy_split(int depth);
 }
 namespace heat::gpu::tbn {  // float2 lanes (tb_narrow.hip)
 bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);

@@ -42,6 +42,7 @@ using heat::gpu::tbdetail::TbArgs;
 using heat::gpu::tbdetail::TbBox;
 using heat::gpu::tbdetail::in_interior;
 using heat::gpu::tbdetail::wave_max_atomic;
+using heat::gpu::tbdetail::kSplitRing;
 
 // Lane 0 (from_left) / lane 63 (from_right) has no source lane and reads 0
 // (bound_ctrl); those lanes lie in the strip overlap, so the value is
@@ -142,7 +143,11 @@ __device__ constexpr int modn(int v) {
 
 // RES: this launch computes the fused residual (check passes only); the
 // other passes get an instantiation without the |delta| max per element.
-template <int K, int LAG, int MODE, bool RES>
+// ROLE (the level-split pipeline, tb_split.hip): 0 = the whole pipeline;
+// 1 = stage 0, levels 1..K of a two-wave pipeline, emitting its last level
+// into the LDS ring of the pair (all lanes, rows [rb, re) of the stage);
+// 2 = stage 1, reading its input rows from that ring instead of memory.
+template <int K, int LAG, int MODE, bool RES, int ROLE = 0>
 struct TbStream {
   static constexpr bool ROWCHK = MODE == kModeGeneric;
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
@@ -156,10 +161,64 @@ struct TbStream {
   unsigned m = 0;
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
   bool nostore = false;  // diagnostics only (kTbDiagNoStore): timing without the stores
+  bool cached_rows = false;  // diagnostics only (kTbDiagCachedRows): loads hit 4 rows
+
+  // Level-split pipeline state (ROLE 1/2): a ring of kSplitRing rows of the
+  // boundary level in LDS, this lane's element of each, plus two counters:
+  // rows produced by stage 0 and rows released by stage 1.
+  vecf* ring = nullptr;           // ring[slot * 64 + lane]
+  unsigned* produced = nullptr;   // LDS, written by stage 0
+  unsigned* released = nullptr;   // LDS, written by stage 1
+  int64_t seq0 = 0;               // row of sequence number 0 (the stage's first_in / rb)
+  unsigned seen = 0;              // last counter value observed (polls only when needed)
+
+  __device__ __forceinline__ vecf load_row(const float* __restrict__ src, int64_t row,
+                                           int64_t pitch) {
+    if constexpr (ROLE == 2) {
+      // Ordering: LDS requests of one wave execute in issue order, so only
+      // the compiler must keep the data access on the right side of the
+      // counter access (asm memory clobbers).  Acquire/release atomics would
+      // also wait for this wave's in-flight global loads and stores (vmcnt)
+      // and serialise the prefetch.
+      const unsigned q = unsigned(row - seq0);
+      if (q >= seen) {
+        unsigned v;
+        while ((v = __hip_atomic_load(produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <= q)
+          __builtin_amdgcn_s_sleep(1);
+        seen = v;
+      }
+      asm volatile("" ::: "memory");
+      const vecf x = ring[(q % kSplitRing) * 64 + (threadIdx.x & 63)];
+      asm volatile("" ::: "memory");
+      // Rows before q are no longer needed (q itself may still be in flight).
+      __hip_atomic_store(released, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return x;
+    } else {
+      if (cached_rows) row = seq0 + (row & 3);  // diagnostics: cache-resident input
+      return *reinterpret_cast<const vecf*>(src + row * pitch);
+    }
+  }
 
   __device__ __forceinline__ void emit(const vecf& out, const vecf& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
                                        int64_t re, bool store_lane) {
+    if constexpr (ROLE == 1) {
+      if (ro >= rb && ro < re) {  // every lane: stage 1 needs the overlap columns too
+        const unsigned q = unsigned(ro - seq0);
+        if (q >= seen + kSplitRing) {  // the slot's previous row may still be unread
+          unsigned v;
+          while ((v = __hip_atomic_load(released, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) +
+                     kSplitRing <= q)
+            __builtin_amdgcn_s_sleep(1);
+          seen = v;
+        }
+        asm volatile("" ::: "memory");
+        ring[(q % kSplitRing) * 64 + (threadIdx.x & 63)] = out;
+        asm volatile("" ::: "memory");  // data before the counter (in-order LDS)
+        __hip_atomic_store(produced, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return;
+    }
     if (ro >= rb && ro < re && store_lane) {
       if (!nostore) *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
       if constexpr (RES) {
@@ -199,10 +258,7 @@ struct TbStream {
       }
     } else {
       R[0][U] = P[Q];
-      {
-        const int64_t nxt = min(i + PF, last_in);
-        P[Q] = *reinterpret_cast<const vecf*>(src + nxt * pitch);
-      }
+      P[Q] = load_row(src, min(i + PF, last_in), pitch);
       // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
       // iterations, so the order below carries no dependency.
 #pragma unroll
@@ -243,7 +299,7 @@ struct TbStream {
       constexpr int U = T % 3, Q = T % PF;
       const int64_t i = first_in + T;
       R[0][U] = P[Q];
-      P[Q] = *reinterpret_cast<const vecf*>(src + min(i + PF, last_in) * pitch);
+      P[Q] = load_row(src, min(i + PF, last_in), pitch);
       ramp_levels<T, 1>(i, rlo, rhi, upd);
       __builtin_amdgcn_sched_barrier(0);
       ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -261,9 +317,9 @@ struct TbStream {
     for (int s = 0; s < K; ++s)
 #pragma unroll
       for (int j = 0; j < RING; ++j) R[s][j] = vecf(0.f);
+    if constexpr (ROLE != 1) seq0 = first_in;
 #pragma unroll
-    for (int j = 0; j < PF; ++j)
-      P[j] = *reinterpret_cast<const vecf*>(src + min(first_in + j, last_in) * pitch);
+    for (int j = 0; j < PF; ++j) P[j] = load_row(src, min(first_in + j, last_in), pitch);
     if constexpr (LAG == 4) {
       // As LAG 3, with the main loop unrolled by 6 for the 6-row prefetch ring.
       ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -326,18 +382,17 @@ constexpr int tb_waves_per_simd() {
   return K <= 2 ? 6 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 8 ? 3 : 2;
 }
 
-template <int K, int LAG>
-__global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
-  constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
-  constexpr int W = 64 * V - 2 * KK;
-  const int lane = threadIdx.x & 63;
+// Grid position -> (work unit, age half); see kTbAgePairs / kTbXcdGroups.
+// `per_block` work units per block (4 waves, or 2 two-wave pipelines).
+__device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, int& age) {
   // Age pairs (kTbAgePairs): the grid is two halves of one block per CU
   // each; a CU runs block i of the first half (dispatched first: the OLDER
   // wave on each SIMD, which the SIMD's issue arbitration favours) next to
   // block i of the second half.  Wave i of both halves takes the same pair
   // of vertically adjacent chunks, the older one the longer share.
   const bool pairs = a.flags & tbdetail::kTbAgePairs;
-  int nb = gridDim.x, blk = blockIdx.x, age = 0;
+  int nb = gridDim.x, blk = blockIdx.x;
+  age = 0;
   if (pairs) {
     nb >>= 1;
     age = blk >= nb;
@@ -347,8 +402,21 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     const int q = nb >> 3, r = nb & 7, x = blk & 7, j = blk >> 3;
     blk = x * q + min(x, r) + j;
   }
-  const int wave = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave >= a.total_waves) return;
+  return blk * per_block + sub;
+}
+
+// One work unit: a (strip, chunk) of the launch's boxes.  K1 = 0: one wave
+// runs all K levels; K1 > 0: a two-wave pipeline, stage 0 levels 1..K1
+// (into the LDS ring), stage 1 levels K1+1..K (`ring`, `cnt`: the pair's
+// LDS ring and its two counters).
+template <int K, int LAG, int K1>
+__device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
+                                       unsigned* cnt) {
+  constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
+  constexpr int W = 64 * V - 2 * KK;
+  constexpr int K2 = K - K1;               // levels of stage 1
+  const int lane = threadIdx.x & 63;
+  const bool pairs = a.flags & tbdetail::kTbAgePairs;
   const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   int bi = 0;
 #pragma unroll
@@ -420,11 +488,32 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     } else if constexpr (MD >= 2) {
       upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
-    TbStream<K, LAG, MD, decltype(res_c)::value> st;
-    st.rc = int(min<int64_t>(cend - col, V));
-    st.nostore = a.flags & tbdetail::kTbDiagNoStore;
-    st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
-    m = st.m;
+    if constexpr (K1 == 0) {
+      TbStream<K, LAG, MD, decltype(res_c)::value> st;
+      st.rc = int(min<int64_t>(cend - col, V));
+      st.nostore = a.flags & tbdetail::kTbDiagNoStore;
+      st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
+      st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
+      m = st.m;
+    } else if (stage == 0) {
+      // Level-K1 rows [rb - K2, re + K2): exactly what stage 1's trapezoid reads.
+      TbStream<K1, LAG, MD, false, 1> st;
+      st.ring = ring;
+      st.produced = cnt;
+      st.released = cnt + 1;
+      st.seq0 = rb - K2;
+      st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
+      st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
+    } else {
+      TbStream<K2, LAG, MD, decltype(res_c)::value, 2> st;
+      st.ring = ring;
+      st.produced = cnt;
+      st.released = cnt + 1;
+      st.rc = int(min<int64_t>(cend - col, V));
+      st.nostore = a.flags & tbdetail::kTbDiagNoStore;
+      st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
+      m = st.m;
+    }
   };
   auto go = [&](auto mode_c) {
     if (want_resid) go2(mode_c, std::true_type{});
@@ -443,9 +532,10 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
       break;
     default: go(std::integral_constant<int, kModeGeneric>{}); break;
   }
-  if (want_resid) wave_max_atomic(m, a.resid);
+  if (want_resid && (K1 == 0 || stage == 1)) wave_max_atomic(m, a.resid);
   if (a.stamps && lane == 0) {
-    unsigned long long* st = a.stamps + 4 * (int64_t(wave) + int64_t(age) * a.total_waves);
+    const int64_t idx = int64_t(wave) + int64_t(age) * a.total_waves;
+    unsigned long long* st = a.stamps + 4 * (K1 == 0 ? idx : 2 * idx + stage);
     st[0] = t_start;
     st[1] = __builtin_amdgcn_s_memrealtime();
     // HW_ID (wave, SIMD, CU, SE ids) and XCC_ID via s_getreg.
@@ -455,6 +545,40 @@ __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(
     st[3] = ((unsigned long long)strip << 32) | unsigned(chunk);
   }
 }
+
+template <int K, int LAG>
+__global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
+  int age = 0;
+  const int wave = tb_unit(a, 4, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), age);
+  if (wave >= a.total_waves) return;
+  tb_run<K, LAG, 0>(a, wave, age, 0, nullptr, nullptr);
+}
+
+#if HEAT_TB_SPLIT
+// Level-split pipeline: a block is two pipelines of two waves; wave 2p runs
+// levels 1..K1 of pipeline p's (strip, chunk), wave 2p+1 levels K1+1..K,
+// fed through an LDS ring.  Same chunks and ramp as one wave doing all K
+// levels, at twice the waves per SIMD (half the ring registers per wave):
+// a lone wave issues a VALU op every ~5 cycles, two ~2.5
+// (profiles/tb_wave_timeline_r1.md).
+template <int K, int K1>
+constexpr int tb_split_waves_per_simd() {
+  return tb_waves_per_simd<(K1 > K - K1 ? K1 : K - K1), 3>();
+}
+template <int K, int K1>
+__global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_split_kernel(TbArgs a) {
+  __shared__ vecf ring[2][kSplitRing * 64];
+  __shared__ unsigned cnt[2][2];
+  if (threadIdx.x < 4) cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __syncthreads();
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = wid >> 1;
+  int age = 0;
+  const int unit = tb_unit(a, 2, p, age);
+  if (unit >= a.total_waves) return;
+  tb_run<K, 3, K1>(a, unit, age, wid & 1, ring[p], cnt[p]);
+}
+#endif
 
 #ifndef HEAT_TB_EXPERIMENT  // experiments instantiate tb_kernel<K, LAG> themselves
 template <int K, int LAG>
@@ -556,5 +680,42 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
   }
 }
 
+#if HEAT_TB_SPLIT
+template <int K, int K1>
+void launch_split_k(const TbArgs& args, hipStream_t st) {
+  int blocks = int((args.total_waves + 1) / 2);  // two pipelines per block
+  if (args.flags & tbdetail::kTbAgePairs) blocks *= 2;
+  hipLaunchKernelGGL((tb_split_kernel<K, K1>), dim3(blocks), dim3(256), 0, st, args);
+}
+template <int K, int K1>
+int occ_split_k() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tb_split_kernel<K, K1>, 256, 0) != hipSuccess)
+    n = 1;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tb_split_kernel<K, K1>)) == hipSuccess &&
+      fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    n = std::min(n, std::min(8, 512 / alloc));
+  }
+  return std::max(1, n);
+}
+// Level-split launches: depth 8 (4 + 4) and 12 (6 + 6).
+bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
+  switch (depth) {
+    case 8: launch_split_k<8, 4>(args, st); return true;
+    case 12: launch_split_k<12, 6>(args, st); return true;
+    default: return false;
+  }
+}
+// Resident blocks per CU (each block = 2 pipelines = 4 waves).
+int occupancy_split(int depth) {
+  switch (depth) {
+    case 8: return occ_split_k<8, 4>();
+    case 12: return occ_split_k<12, 6>();
+    default: return 1;
+  }
+}
+#endif
 #endif  // HEAT_TB_EXPERIMENT
 }  // namespace heat::gpu::HEAT_TB_NS

@@ -64,10 +64,13 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant,depth", [(7, 12), (23, 12), (55, 12), (279, 12)])
+@pytest.mark.parametrize("variant,depth", [(7, 12), (23, 12), (55, 12), (279, 12),
+                                           (2055, 8), (2071, 8), (2071, 12), (2103, 12),
+                                           (2327, 12)])
 def test_tb_deep_bitwise_vs_cpu_oracle(gpu, depth, variant):
     # Depth 12 exists in the scalar ring-3+ramp build only (+32 mirrored odd
-    # chunks, +256 age pairs).
+    # chunks, +256 age pairs); +2048: two-wave level-split pipelines
+    # (depths 8 and 12) fed through the LDS ring.
     lx, ly = 203, 517
     g, a, b = _fields(lx, ly, depth, gpu)
     ops.tb_step(a, b, g, depth, variant=variant)
@@ -93,7 +96,7 @@ def test_tb_age_pairs_bitwise(gpu, depth, variant, waves):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant", [7, 55, 87])
+@pytest.mark.parametrize("variant", [7, 55, 87, 2071])
 @pytest.mark.parametrize("waves", [64, 4096])
 def test_tb_chunking_invariance(gpu, waves, variant):
     lx, ly, k = 300, 1000, 8
@@ -120,13 +123,22 @@ def test_tb_subdomain_offsets_and_boxes(gpu):
     torch.cuda.synchronize()
     full = _cpu_steps(ops.Geom(nx=NX, ny=NY), NX, NY, 1, k, seed=5)
     assert torch.equal(b.owned().cpu(), full[ox:ox + lx, oy:oy + ly])
+    c = ops.Field(lx, ly, 8, gpu)
+    d = ops.Field(lx, ly, 8, gpu)
+    ops.init_field(c, g, "random", 5)
+    ops.init_field(d, g, "random", 5)
+    ops.tb_step(c, d, g, 8, boxes=[(0, lx, 0, 296), (0, lx, 296, ly)], variant=2071)
+    torch.cuda.synchronize()
+    full8 = _cpu_steps(ops.Geom(nx=NX, ny=NY), NX, NY, 1, 8, seed=5)
+    assert torch.equal(d.owned().cpu(), full8[ox:ox + lx, oy:oy + ly])
 
 
-def test_tb_residual(gpu):
-    lx, ly, k = 64, 300, 4
+@pytest.mark.parametrize("k,variant", [(4, -1), (8, 2071), (12, 2071)])
+def test_tb_residual(gpu, k, variant):
+    lx, ly = 64, 300
     g, a, b = _fields(lx, ly, k, gpu)
     resid = torch.zeros(1, dtype=torch.int32, device=gpu)
-    ops.tb_step(a, b, g, k, resid=resid)
+    ops.tb_step(a, b, g, k, resid=resid, variant=variant)
     torch.cuda.synchronize()
     prev = _cpu_steps(g, lx, ly, k, k - 1)
     last = _cpu_steps(g, lx, ly, k, k)
