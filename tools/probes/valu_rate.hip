@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float a, flo
   if constexpr (KIND == 11) asm("v_mov_b32 %0, %1" : "=v"(b) : "s"(b));
   float cf[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) asm("v_mov_b32 %0, %1" : "=v"(cf[q]) : "s"(b));
+  for (int q = 0; q < 4; ++q) asm volatile("v_mov_b32 %0, %1" : "=v"(cf[q]) : "s"(b));
   float v[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) v[j] = float(threadIdx.x + j);
