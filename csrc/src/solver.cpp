@@ -78,7 +78,10 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
   // each computing the still-valid part of the ghost ring redundantly.
   int m = 1;
   if (sched_ == Schedule::Sync && world > 1) {
-    m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 4) : 1);
+    // m = 8 (H = 64 rows at K = 8, 96 at K = 12): larger m trades a few
+    // percent of redundant ghost compute for fewer exchanges, whose
+    // latency dominates on small blocks (profiles/halo_passes_r1.md).
+    m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 8) : 1);
     m = int(std::max<int64_t>(1, std::min<int64_t>(m, min_ext / T_)));
   }
   H_ = m * T_;
