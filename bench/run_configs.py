@@ -91,7 +91,7 @@ def main():
             elif c == 5 and (ng >= 8 or (a.capacity_1gpu and ng >= 1)):
                 n = 8 if ng >= 8 else 1
                 d = run(bench(n, ["--nx", "131072", "--ny", "131072", "--converge",
-                                  "--check-interval", "50", "--steps", "1", "--warmup", "0",
+                                  "--check-interval", "50", "--steps", "1", "--warmup", "1",
                                   "--iters-per-step", "200"]), timeout=5000)
                 name = f"c5_131072_{n}gpu_conv50"
             else:
