@@ -21,6 +21,23 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float a, flo
 #pragma unroll
   for (int j = 0; j < NCH; ++j) v[j] = float(threadIdx.x + j);
   for (int it = 0; it < iters; ++it) {
+    if constexpr (KIND == 14) {  // DPP add whose result feeds the next instruction
+#pragma unroll
+      for (int j = 0; j < NCH; j += 2) {
+        const float t = v[j] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[(j + 5) % NCH]), 0x138, 0xf, 0xf, true));
+        v[j] = __builtin_fmaf(t, -2.0f, v[(j + 1) % NCH]);
+      }
+      continue;
+    }
+    if constexpr (KIND == 15) {  // the same ops, DPP results consumed 8 instructions later
+      float t[NCH / 2];
+#pragma unroll
+      for (int j = 0; j < NCH; j += 2)
+        t[j / 2] = v[j] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[(j + 5) % NCH]), 0x138, 0xf, 0xf, true));
+#pragma unroll
+      for (int j = 0; j < NCH; j += 2) v[j] = __builtin_fmaf(t[j / 2], -2.0f, v[(j + 1) % NCH]);
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       if constexpr (KIND == 0) {  // v_fmac_f32 (2 VGPR + SGPR)
@@ -92,9 +109,10 @@ int main() {
                          "v_pk_fma_f32", "v_fmac_f32 (v,s,v)", "v_fmac_f32 (v,-2.0,v)", "v_fma_f32 (v,s,v,v)",
                          "v_fmac_f32 operands +4,+8 regs", "v_fmac_f32 operands +1,+2 regs",
                          "v_fma_f32 (v,v,v,v) VOP3", "v_fmac_f32 (v, vgpr coef, v)",
-                         "v_fmac_f32 (v, 0.1 literal, v)", "v_fmac_f32 (v, 4 vgpr coef copies, v)"};
-  const int per_body[] = {NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH};
-  for (int kind = 0; kind < 14; ++kind) {
+                         "v_fmac_f32 (v, 0.1 literal, v)", "v_fmac_f32 (v, 4 vgpr coef copies, v)",
+                         "dpp add -> dependent fma (8+8 per iter)", "dpp adds then fmas (8+8 per iter)"};
+  const int per_body[] = {NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH, NCH};
+  for (int kind = 0; kind < 16; ++kind) {
     for (int w : {1, 2, 3, 4}) {
       double ms = 0;
       switch (kind) {
@@ -112,6 +130,8 @@ int main() {
         case 11: ms = run<11>(w, cus, iters, out); break;
         case 12: ms = run<12>(w, cus, iters, out); break;
         case 13: ms = run<13>(w, cus, iters, out); break;
+        case 14: ms = run<14>(w, cus, iters, out); break;
+        case 15: ms = run<15>(w, cus, iters, out); break;
       }
       // instructions per SIMD = waves/SIMD x iters x body
       const double instr = double(w) * iters * per_body[kind];
