@@ -80,6 +80,7 @@ struct Chain {
           ws[s - 1] = from_left(b.w);
           es[s - 1] = from_right(b.x);
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the shifts grouped
         R[p][0][U] = in[p];
 #pragma unroll
         for (int s = 1; s < K; ++s)
@@ -157,7 +158,5 @@ int main() {
   run<8, 1, 0>(cus, clk);
   run<8, 1, 1>(cus, clk);
   run<8, 1, 16>(cus, clk);
-  run<12, 1, 0>(cus, clk);
-  run<12, 1, 16>(cus, clk);
   return 0;
 }
