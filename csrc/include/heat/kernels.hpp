@@ -81,7 +81,8 @@ void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& bo
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
-int tb_default_variant();
+// Variant a launch of `depth` uses by default (HEAT_TB_VARIANT overrides).
+int tb_default_variant(int depth);
 // Diagnostics: while set, every tb_step launch writes 4 u64 per wave into buf
 // ({start, end} s_memrealtime ticks (100 MHz), block, strip<<32 | chunk);
 // waves = buffer capacity in waves.  nullptr switches it off.

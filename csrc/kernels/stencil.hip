@@ -247,13 +247,18 @@ int tb_resident_waves(int depth, int variant) {
   return w;
 }
 
-int tb_default_variant() {
-  static const int v = [] {
+int tb_default_variant(int depth) {
+  static const int env = [] {
     const char* e = std::getenv("HEAT_TB_VARIANT");
-    // ring-3 + ramp skip, scalar build, XCD-grouped blocks (tools/tb_sweep.py)
-    return e && *e ? std::atoi(e) : 23;
+    return e && *e ? std::atoi(e) : -1;
   }();
-  return v;
+  if (env >= 0) return env;
+  // Ring-3 + ramp skip, scalar build, XCD-grouped blocks (23); at depth 12
+  // (tall blocks) as two-wave level-split pipelines with ds_bpermute lane
+  // shifts (2071): +5 % in bench.py, +9-10 % in the interleaved kernel A/B
+  // (profiles/tb_wave_timeline_r1.md).  On the short slabs of many-GPU runs
+  // (depth 8) the split form loses, so 23 stays.
+  return depth == kTbDeepDepth ? 2071 : 23;
 }
 
 void init_field(float* origin, const Layout& L, int64_t gx0, int64_t gy0, int64_t nx, int64_t ny,
@@ -287,7 +292,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
-  if (variant < 0) variant = tb_default_variant();
+  if (variant < 0) variant = tb_default_variant(depth);
   const int lag = tb_variant_lag(variant);
   const int W = tb_strip_width(depth, tb_lane_cols(variant));
   int64_t total_strip_rows = 0;

@@ -49,12 +49,28 @@ using heat::gpu::tbdetail::kSplitRing;
 // don't-care.  bound_ctrl lets the compiler fold both shifts into the
 // consuming v_add_f32_dpp; with old = 0 and bound_ctrl off it only folded
 // wave_shr and materialised wave_shl as v_mov 0 + v_mov_b32_dpp + v_add.
+#if HEAT_TB_BPERMUTE
+// Lane shifts through the LDS crossbar (ds_bpermute_b32, no LDS memory):
+// DPP wave shifts mixed into the FMA stream stop a second wave per SIMD from
+// adding throughput (tools/probes/stencil_chain.hip: ~105 cycles per float4
+// row update at 1-4 waves; with ds_bpermute 82 at 2 waves, 71 at 4).  Lane
+// 0 / 63 wrap around; they lie in the strip overlap (don't-care).
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane l <- lane l-1
+  const int l = threadIdx.x & 63;
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 63) & 63) << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+1
+  const int l = threadIdx.x & 63;
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 1) & 63) << 2, __float_as_int(v)));
+}
+#else
 __device__ __forceinline__ float dpp_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float dpp_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
+#endif
 
 // A wave-uniform value moved into a VGPR.  A VALU instruction with an SGPR
 // operand issues at half rate on gfx950 (tools/probes/valu_rate.hip:

@@ -220,7 +220,7 @@ int Solver::auto_tb_depth() const {
   // the shorter chunks costs more than the bytes it saves
   // (profiles/tb_depth_sweep_r1.md).  Decided from the smallest block of any
   // rank, so every rank picks the same depth.
-  if (!gpu::tb_variant_deep(gpu::tb_default_variant())) return 8;
+  if (!gpu::tb_variant_deep(gpu::tb_default_variant(gpu::kTbDeepDepth))) return 8;
   int64_t min_lx = INT64_MAX;
   for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
   return min_lx >= 3072 ? gpu::kTbDeepDepth : 8;
