@@ -154,8 +154,11 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             waves_target: int = 0, variant: int = -1) -> None:
     """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes.
 
-    variant: -1 default; bits 0-1 pipeline (0 ring-3, 1 ring-4 skew-2, 2 ring-2 + copy),
-    bit 2 the scalar build.
+    variant: -1 default (23 at depth <= 8, 2071 at depth 12); bits 0-1 pipeline
+    (0 ring-3, 1 ring-4 skew-2, 2 ring-2 + copy, 3 ring-3 + ramp), bit 2 the scalar
+    build, 16 XCD-grouped blocks, 32 odd chunks bottom-up, 64 float2 lanes,
+    256 age-paired chunks, 2048 two-wave level-split pipelines (depths 8/12),
+    diagnostics (wrong results): 1024 no stores, 4096 cache-resident input rows.
     """
     if src.device.type == "cpu":
         raise ValueError("tb_step is a GPU kernel")
