@@ -215,15 +215,16 @@ int64_t Solver::configured_steps(int64_t steps) const {
 }
 
 int Solver::auto_tb_depth() const {
-  // Depth 12 (2/3 the HBM bytes per update of 8, at 2 waves/SIMD) wins on
-  // tall blocks and loses a little below ~3K rows, where the longer ramp of
-  // the shorter chunks costs more than the bytes it saves
-  // (profiles/tb_depth_sweep_r1.md).  Decided from the smallest block of any
-  // rank, so every rank picks the same depth.
+  // Depth 12 (2/3 the HBM bytes per update of 8; the level-split pipelines
+  // of tb_default_variant) wins from 2048-row blocks up (+5 % there, +10 %
+  // at 4096+), depth 8 on 1024-row blocks, where the longer ramp of the
+  // shorter chunks costs more than the bytes it saves
+  // (profiles/tb_depth_sweep_r1.md, tb_small_slab_sweep_r1.jsonl).  Decided
+  // from the smallest block of any rank, so every rank picks the same depth.
   if (!gpu::tb_variant_deep(gpu::tb_default_variant(gpu::kTbDeepDepth))) return 8;
   int64_t min_lx = INT64_MAX;
   for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
-  return min_lx >= 3072 ? gpu::kTbDeepDepth : 8;
+  return min_lx >= 2048 ? gpu::kTbDeepDepth : 8;
 }
 
 std::vector<int> Solver::pass_depths(int64_t n) const {
