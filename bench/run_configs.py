@@ -10,7 +10,13 @@ one JSON line per config to bench/results/<name>.json.
      with --capacity-1gpu the same grid also runs on ONE GPU: 2 x 68.7 GB fits
      in 288 GB HBM3E)
 
-Usage: python bench/run_configs.py [--configs 1,2] [--capacity-1gpu]
+With --rehearse-1gpu, configs 3 and 4 run at full size on ONE GPU as N ranks
+that are threads of one process (`heat --gpus N`, loopback transport: the same
+message list and device-memory halo buffers as RCCL, moved by D2D copies).
+That checks the decomposition, deep halos, schedules and graphs end to end on
+real hardware; its throughput is one GPU's, not an N-GPU number.
+
+Usage: python bench/run_configs.py [--configs 1,2] [--capacity-1gpu] [--rehearse-1gpu]
 Multi-GPU configs are launched with torch.distributed.run (one rank per GPU).
 """
 import argparse
@@ -65,6 +71,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,3,4,5")
     ap.add_argument("--capacity-1gpu", action="store_true")
+    ap.add_argument("--rehearse-1gpu", action="store_true")
     a = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     ng = gpus()
@@ -84,6 +91,18 @@ def main():
                 d = run(bench(2, ["--nx", "16384", "--ny", "16384", "--decomp", "rows",
                                   "--steps", "5", "--warmup", "1"]))
                 name = "c3_16384_2gpu_1d"
+            elif c in (3, 4) and a.rehearse_1gpu and ng >= 1:
+                cli = os.path.join(ROOT, "build", "heat")
+                if c == 3:
+                    extra = ["--gpus", "2", "--nx", "16384", "--ny", "16384", "--decomp", "rows"]
+                    name = "c3_16384_2ranks_rehearsal_1gpu"
+                else:
+                    extra = ["--gpus", "8", "--nx", "32768", "--ny", "32768", "--decomp", "2d",
+                             "--schedule", "overlap"]
+                    name = "c4_32768_8ranks_2d_overlap_rehearsal_1gpu"
+                d = run([cli] + extra + ["--steps", "1000", "--init", "random", "--seed", "1234",
+                                         "--out", "none", "--json"])
+                d["note"] = "N ranks as threads on ONE GPU (loopback transport); not an N-GPU number"
             elif c == 4 and ng >= 8:
                 d = run(bench(8, ["--nx", "32768", "--ny", "32768", "--decomp", "2d",
                                   "--steps", "3", "--warmup", "1"]))
