@@ -55,7 +55,8 @@ void usage() {
       "  --resume PATH           start from a binary checkpoint\n"
       "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
       "  --port P                rendezvous port (default MASTER_PORT+1 or 29600)\n"
-      "  --gpus N                one process, N GPU ranks as threads (loopback/peer copies)\n"
+      "  --gpus N                one process, N GPU ranks as threads (loopback/peer copies;\n"
+      "                          with --transport rccl: one RCCL rank per GPU)\n"
       "  --phase-timing          per-phase times (exchange/compute/reduce) in --json; eager\n"
       "  --json                  print a JSON metrics line\n");
 }
@@ -319,7 +320,21 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "heat: --gpus needs the hip backend\n");
       return 2;
     }
-    LoopbackHub* hub = loopback_hub_create(gpus);
+    // `--transport rccl`: one RCCL communicator rank per thread, one GPU
+    // each (the ncclCommInitAll process model of SURVEY R10; RCCL refuses two
+    // ranks on one device, so it needs `gpus` visible GPUs).
+    const bool rccl = transport == "rccl";
+    if (rccl && gpus > ndev) {
+      std::fprintf(stderr, "heat: --gpus %d --transport rccl needs %d GPUs, %d visible\n", gpus,
+                   gpus, ndev);
+      return 2;
+    }
+    unsigned char uid[128] = {0};
+    LoopbackHub* hub = nullptr;
+    if (rccl)
+      rccl_unique_id(uid);
+    else
+      hub = loopback_hub_create(gpus);
     std::vector<std::thread> threads;
     std::vector<std::string> errors(gpus);
     for (int r = 0; r < gpus; ++r)
@@ -327,13 +342,17 @@ int main(int argc, char** argv) {
         try {
           Params Pr = P;
           Pr.device = r % ndev;
-          run_rank(o, Pr, make_loopback_transport(hub, r, Pr.device));
+          // ncclCommInitRank blocks until every rank joined: each rank
+          // initialises on its own thread, concurrently.
+          run_rank(o, Pr,
+                   rccl ? make_rccl_transport(r, gpus, uid, Pr.device)
+                        : make_loopback_transport(hub, r, Pr.device));
         } catch (const std::exception& e) {
           errors[r] = e.what();
         }
       });
     for (auto& t : threads) t.join();
-    loopback_hub_destroy(hub);
+    if (hub) loopback_hub_destroy(hub);
     for (int r = 0; r < gpus; ++r)
       if (!errors[r].empty()) {
         std::fprintf(stderr, "heat: rank %d error: %s\n", r, errors[r].c_str());

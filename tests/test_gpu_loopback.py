@@ -107,6 +107,34 @@ def test_cli_single_process_gpus(gpu, tmp_path):
     assert outs[3][1]["ranks"] == 3 and outs[3][1]["transport"] == "loopback"
 
 
+def test_cli_single_process_rccl(gpu, tmp_path):
+    # `heat --gpus N --transport rccl`: one RCCL rank per thread and GPU.  With
+    # fewer GPUs than ranks it must refuse cleanly (RCCL rejects two ranks on
+    # one device); with enough GPUs it must match the 1-rank hash.
+    import json
+    import subprocess
+
+    import torch
+
+    from parallel_heat_amd import _native
+    ndev = torch.cuda.device_count()
+    args = ["--backend", "hip", "--nx", "130", "--ny", "90", "--steps", "37", "--init",
+            "random", "--out", "c.json", "--out-format", "checksum", "--json"]
+    if ndev < 2:
+        p = subprocess.run([str(_native.CLI_PATH), "--gpus", "2", "--transport", "rccl"] + args,
+                           cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert p.returncode == 2 and "needs 2 GPUs" in p.stderr
+        return
+    hashes = {}
+    for n in (1, 2):
+        d = tmp_path / f"g{n}"
+        d.mkdir()
+        subprocess.run([str(_native.CLI_PATH), "--gpus", str(n), "--transport", "rccl"] + args,
+                       cwd=d, capture_output=True, text=True, timeout=300, check=True)
+        hashes[n] = json.loads((d / "c.json").read_text())["hash"]
+    assert hashes[2] == hashes[1]
+
+
 def test_loopback_phase_timing(gpu):
     cfg = HeatConfig(**{**BASE, "decomp": "rows", "phase_timing": True, "converge": True,
                         "check_interval": 16})
