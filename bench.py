@@ -83,7 +83,19 @@ def main() -> int:
                      overlap=not args.no_overlap, device=local_rank % torch.cuda.device_count(),
                      schedule=args.schedule, halo_passes=args.halo_passes,
                      phase_timing=args.phase_timing)
-    solver = HeatSolver(cfg, dist_info=DistInfo(rank, world, local_rank))
+    info = DistInfo(rank, world, local_rank)
+    try:
+        solver = HeatSolver(cfg, dist_info=info)
+    except Exception as e:  # noqa: BLE001
+        if world == 1:
+            raise
+        # The engine's own RCCL communicator failed to come up on every rank:
+        # fall back, loudly, to halos staged through host memory over a gloo
+        # group (the transport name lands in config.parallelism).
+        print(f"[bench] rank {rank}: RCCL transport failed ({e}); "
+              "falling back to the staged torch/gloo transport", file=sys.stderr, flush=True)
+        solver = HeatSolver(cfg, transport="torch", dist_info=info,
+                            group=dist.new_group(backend="gloo"))
 
     def barrier():
         if world > 1:

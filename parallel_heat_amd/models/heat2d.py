@@ -83,7 +83,7 @@ class HeatSolver:
 
     def __init__(self, config: HeatConfig, transport: str = "auto",
                  dist_info: Optional[pcomm.DistInfo] = None, device: Optional[int] = None,
-                 hub: Optional[pcomm.LoopbackHub] = None):
+                 hub: Optional[pcomm.LoopbackHub] = None, group=None):
         self.config = config
         config.validate()
         if config.backend == "hip":
@@ -107,7 +107,7 @@ class HeatSolver:
         self.device = device
         self.transport = transport
         self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0),
-                                                 hub=hub)
+                                                 hub=hub, group=group)
         params = config.to_native(device=device)
         h = ctypes.c_void_p()
         _native.call("heat_solver_create", ctypes.byref(params), ctypes.byref(self._comm),

@@ -173,8 +173,11 @@ class LoopbackHub:
 
 
 def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = None,
-              port: Optional[int] = None, hub: Optional[LoopbackHub] = None):
-    """Build a native HeatComm (and the Python object that must outlive it)."""
+              port: Optional[int] = None, hub: Optional[LoopbackHub] = None, group=None):
+    """Build a native HeatComm (and the Python object that must outlive it).
+
+    `group`: torch.distributed process group of the ``torch`` transport
+    (default: the default group; it must support CPU tensors, e.g. gloo)."""
     comm = _native.HeatComm()
     keep = None
     if kind == "loopback":
@@ -194,7 +197,7 @@ def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = 
         comm.rank, comm.world, comm.device = info.rank, info.world, device
         ctypes.memmove(comm.unique_id, uid, 128)
     elif kind == "torch":
-        keep = TorchDistTransport()
+        keep = TorchDistTransport(group)
         keep.fill(comm)
     elif kind == "tcp":
         comm.kind = 2

@@ -29,8 +29,11 @@ def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
     from parallel_heat_amd.parallel.comm import DistInfo
 
     cfg = HeatConfig(**cfg_kwargs)
+    group = None
+    if transport == "torch_subgroup":  # bench.py's fallback: an explicit gloo group
+        transport, group = "torch", dist.new_group(backend="gloo")
     s = HeatSolver(cfg, transport=transport, dist_info=DistInfo(rank, world, rank),
-                   device=0 if cfg.backend == "hip" else None)
+                   device=0 if cfg.backend == "hip" else None, group=group)
     if cfg_kwargs.get("init") == "zero":  # start from a grid scattered by rank 0
         from parallel_heat_amd.models import reference as R
         s.scatter(R.init_grid(cfg.nx, cfg.ny, "random", 77) if rank == 0 else None)

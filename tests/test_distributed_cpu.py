@@ -65,6 +65,15 @@ def test_invariance_chunked_runs(tmp_path):
     assert np.array_equal(res["grid"], ref)
 
 
+def test_explicit_gloo_group(tmp_path):
+    # HeatSolver(..., transport="torch", group=<gloo group>): bench.py's
+    # fallback when the engine's RCCL communicator cannot be created.
+    kw = {**BASE, "tb_depth": 2}
+    res = run_world(2, kw, 19, tmp_path, transport="torch_subgroup")
+    ref, _ = single(BASE, 19)
+    assert np.array_equal(res["grid"], ref)
+
+
 def test_convergence_distributed(tmp_path):
     kw = dict(nx=24, ny=30, steps=20000, converge=True, check_interval=20, eps=1e-3,
               backend="cpu", tb_depth=2)
