@@ -91,7 +91,7 @@ ref-variants: $(BUILD)/heat
 	          "heat_con_$(SIZE):--threads 1 --converge --check-interval $(STEP)" \
 	          "heat_con_omp_$(SIZE):--threads $(THREADS) --converge --check-interval $(STEP)"; do \
 	  name=$${v%%:*}; args=$${v#*:}; \
-	  printf '#!/bin/bash\n# %s: reference mpi/Makefile variant\nexec python3 -m torch.distributed.run --no-python --standalone --nproc-per-node $${NP:-1} %s --backend cpu --nx %s --ny %s --steps %s --naming mpi %s "$$@"\n' \
+	  printf '#!/bin/bash\n# %s: reference mpi/Makefile variant\nexec python3 -m torch.distributed.run --no-python --standalone --local-addr 127.0.0.1 --nproc-per-node $${NP:-1} %s --backend cpu --nx %s --ny %s --steps %s --naming mpi %s "$$@"\n' \
 	    "$$name" "$(abspath $(BUILD)/heat)" $(SIZE) $(SIZE) $(STEPS) "$$args" > $(BUILD)/ref/$$name; \
 	  chmod +x $(BUILD)/ref/$$name; done
 	@printf '#!/bin/bash\n# cuda_heat: reference cuda/Makefile program\nexec %s --backend hip --nx %s --ny %s --steps %s --naming cuda "$$@"\n' \

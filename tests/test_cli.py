@@ -138,3 +138,28 @@ def test_python_cli_torchrun_gloo(tmp_path):
     g = hio.read_dat(str(tmp_path / "g.dat"))
     ref = reference_grid(33, 21, 40, init="random")
     assert np.allclose(g, np.round(ref, 1), atol=0.051)
+
+
+def test_make_ref_variants_wrappers(tmp_path):
+    """R21: `make ref-variants` writes the reference's mpi/Makefile program names
+    (mpi/Makefile:12-22) as wrappers over `heat`; NP=1 and NP=2 (torchrun
+    ranks over TCP, 127.0.0.1) give byte-identical final_im.dat."""
+    subprocess.run(["make", "-s", "-C", ROOT, "ref-variants", "SIZE=40", "STEPS=60", "STEP=10",
+                    "THREADS=2"], check=True, capture_output=True, timeout=600)
+    ref_dir = os.path.join(os.path.dirname(HEAT), "ref")
+    for name in ("heat_40", "heat_omp_40", "heat_con_40", "heat_con_omp_40", "cuda_heat"):
+        assert os.access(os.path.join(ref_dir, name), os.X_OK), name
+    outs = {}
+    for np_ in ("1", "2"):
+        d = tmp_path / f"np{np_}"
+        d.mkdir()
+        p = subprocess.run([os.path.join(ref_dir, "heat_omp_40")], cwd=d, capture_output=True,
+                           text=True, timeout=300, env=dict(os.environ, NP=np_))
+        assert p.returncode == 0, p.stderr[-3000:]
+        assert f"Starting mpi_heat2D with {np_} worker tasks." in p.stdout
+        outs[np_] = (d / "final_im.dat").read_bytes()
+    assert outs["1"] == outs["2"]
+    p = subprocess.run([os.path.join(ref_dir, "heat_con_omp_40")], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, NP="2"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "converged" in p.stdout
