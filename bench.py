@@ -16,10 +16,25 @@ Data: synthetic random-init temperature grid (--init random), no files.
 Timing: W untimed warmup steps, then barrier + synchronize, K timed steps,
 synchronize + barrier; the max over ranks is reported.  Everything the model
 does per iteration (halo exchange, all kernels) is inside the timed region.
+
+Verification (after the timed region, `--no-verify` skips it): the global
+checksum of the final state is compared with the same number of steps of a
+single-rank run of the independent LDS-tiled single-step kernel on rank 0's GPU
+(bitwise-equal numerics): `"verified": true` in the JSON line means the
+benchmarked (multi-GPU, graph-captured, temporally blocked) run computed
+exactly the reference field.  A mismatch prints `"verified": false` and exits
+non-zero.
+
+Failure handling: RCCL must come up on every rank (the ranks agree through
+torch.distributed before going on); if it fails anywhere the run exits
+non-zero, unless `--allow-fallback` lets ALL ranks switch together to halos
+staged through host memory (named in config.parallelism).  A watchdog ends a
+hung run with a stack dump instead of letting it hang (`--watchdog-s`).
 """
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -30,6 +45,10 @@ import torch.distributed as dist
 
 BASELINE_MCELLS = 3556.2  # reference best single-GPU throughput (Heat.pdf p.11 Table 6, 1000^2 T=8)
 METRIC = "Mcells/sec (whole node) + sec/1000 iters, 8192^2 grid at 1/2/4/8 MI355X"
+
+
+def log(rank: int, msg: str) -> None:
+    print(f"[bench] rank {rank}: {msg}", file=sys.stderr, flush=True)
 
 
 def main() -> int:
@@ -55,6 +74,12 @@ def main() -> int:
     ap.add_argument("--halo-passes", type=int, default=0)
     ap.add_argument("--phase-timing", action="store_true",
                     help="diagnostic: eager run with per-phase device times (not the headline)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-run check against a single-rank LDS-kernel run")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="if RCCL fails on every rank, run with host-staged halos over gloo")
+    ap.add_argument("--watchdog-s", type=float, default=900.0,
+                    help="abort (stack dump, exit 1) if one phase takes longer than this")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -63,12 +88,23 @@ def main() -> int:
     if args.weak:
         args.nx *= world
     if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-              file=sys.stderr)
+        log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
-        print("[bench] no GPU visible", file=sys.stderr)
+        log(rank, "no GPU visible")
         return 1
-    torch.cuda.set_device(local_rank % torch.cuda.device_count())
+
+    def watchdog(phase: str, seconds: float) -> None:
+        # A hung collective (a peer that died, a stuck exchange) ends the
+        # process with every thread's stack instead of hanging the job.
+        faulthandler.cancel_dump_traceback_later()
+        if seconds > 0:
+            if args.verbose:
+                log(rank, f"phase {phase} (watchdog {seconds:.0f} s)")
+            faulthandler.dump_traceback_later(seconds, exit=True)
+
+    watchdog("init", args.watchdog_s)
+    device = local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
@@ -80,31 +116,46 @@ def main() -> int:
                      backend="hip", kernel=args.kernel, tb_depth=args.tb_depth,
                      decomp=args.decomp, converge=args.converge,
                      check_interval=args.check_interval, use_graph=not args.no_graph,
-                     overlap=not args.no_overlap, device=local_rank % torch.cuda.device_count(),
+                     overlap=not args.no_overlap, device=device,
                      schedule=args.schedule, halo_passes=args.halo_passes,
                      phase_timing=args.phase_timing)
     info = DistInfo(rank, world, local_rank)
+
+    solver = None
     try:
         solver = HeatSolver(cfg, dist_info=info)
-    except Exception as e:  # noqa: BLE001
+    except _native.NativeError as e:
         if world == 1:
             raise
-        # The engine's own RCCL communicator failed to come up on every rank:
-        # fall back, loudly, to halos staged through host memory over a gloo
-        # group (the transport name lands in config.parallelism).
-        print(f"[bench] rank {rank}: RCCL transport failed ({e}); "
-              "falling back to the staged torch/gloo transport", file=sys.stderr, flush=True)
-        solver = HeatSolver(cfg, transport="torch", dist_info=info,
-                            group=dist.new_group(backend="gloo"))
+        log(rank, f"RCCL transport failed: {e}")
+    if world > 1:
+        # Every rank must agree on the transport before the first exchange:
+        # a rank whose communicator failed would otherwise leave its peers
+        # blocked in RCCL.  torch's own process group carries the vote.
+        ok = torch.tensor([1 if solver is not None else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if solver is not None:
+                solver.close()
+                solver = None
+            if not args.allow_fallback:
+                log(rank, "RCCL transport unavailable on some rank; exiting "
+                          "(--allow-fallback runs host-staged halos over gloo instead)")
+                return 1
+            log(rank, "falling back to host-staged halos over gloo (all ranks)")
+            solver = HeatSolver(cfg, transport="torch", dist_info=info,
+                                group=dist.new_group(backend="gloo"))
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    watchdog("warmup", args.watchdog_s)
     for _ in range(args.warmup):
         solver.run(args.iters_per_step)
     barrier()
     torch.cuda.synchronize()
+    watchdog("timed", args.watchdog_s)
     t0 = time.perf_counter()
     done = 0
     phases = [0.0, 0.0, 0.0]
@@ -119,6 +170,13 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+
+    verified = None
+    check = {}
+    if not args.no_verify:
+        watchdog("verify", args.watchdog_s)
+        verified, check = verify(solver, cfg, rank, world, device, HeatSolver, DistInfo)
+    faulthandler.cancel_dump_traceback_later()
 
     cells = args.nx * args.ny * done
     mcells = cells / elapsed / 1e6
@@ -149,7 +207,10 @@ def main() -> int:
                                f"halo {solver.info.halo}, schedule {solver.info.schedule}",
                 "converge_check": bool(args.converge),
             },
+            "verified": verified,
         }
+        if check:
+            line["verification"] = check
         if args.verbose:
             line["native"] = _native.loaded_path()
         if args.phase_timing:
@@ -160,7 +221,37 @@ def main() -> int:
     solver.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return 0 if verified is not False else 2
+
+
+def verify(solver, cfg, rank, world, device, HeatSolver, DistInfo):
+    """Global checksum of the benchmarked state vs rank 0's single-rank run of
+    the same steps with the LDS-tiled single-step kernel (an independent
+    kernel, bitwise equal to the CPU oracle).  Collective; returns the verdict
+    on every rank and a small record for the JSON line."""
+    steps = solver.step
+    got = solver.checksum()  # collective (all-reduced over the ranks)
+    ok = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rec = {}
+    if rank == 0:
+        t0 = time.perf_counter()
+        ref_cfg = cfg.replace(kernel="lds", tb_depth=0, converge=False, phase_timing=False)
+        with HeatSolver(ref_cfg, transport="local", dist_info=DistInfo(0, 1, 0),
+                        device=device) as ref:
+            left = steps
+            while left > 0:  # 1000-step segments: one captured graph, replayed
+                left -= ref.run(min(1000, left)).steps_done
+            want = ref.checksum()
+        ok[0] = int(got["hash"] == want["hash"] and got["count"] == want["count"])
+        rec = {"steps": steps, "hash": got["hash"], "reference_hash": want["hash"],
+               "reference": "1 rank, lds kernel", "seconds": round(time.perf_counter() - t0, 3)}
+        if not ok[0]:
+            print(f"[bench] VERIFICATION FAILED after {steps} steps: hash {got['hash']} "
+                  f"(sum {got['sum']}) vs single-rank lds {want['hash']} (sum {want['sum']})",
+                  file=sys.stderr, flush=True)
+    if world > 1:
+        dist.broadcast(ok, src=0)
+    return bool(ok.item()), rec
 
 
 if __name__ == "__main__":

@@ -349,15 +349,30 @@ int main(int argc, char** argv) {
                         : make_loopback_transport(hub, r, Pr.device));
         } catch (const std::exception& e) {
           errors[r] = e.what();
+          if (hub) {
+            // Loopback peers blocked on this rank's messages throw in turn.
+            loopback_hub_fail(hub);
+          } else {
+            // RCCL peers would block forever in ncclGroupEnd / collectives
+            // waiting for this rank: report and end the process now.
+            std::fprintf(stderr, "heat: rank %d error: %s\n", r, e.what());
+            std::fflush(stderr);
+            std::_Exit(1);
+          }
         }
       });
     for (auto& t : threads) t.join();
     if (hub) loopback_hub_destroy(hub);
-    for (int r = 0; r < gpus; ++r)
-      if (!errors[r].empty()) {
-        std::fprintf(stderr, "heat: rank %d error: %s\n", r, errors[r].c_str());
-        return 1;
-      }
+    // Report the failing rank, not the peers it unblocked.
+    int first = -1;
+    for (int r = 0; r < gpus && first < 0; ++r)
+      if (!errors[r].empty() && errors[r].find("a peer rank failed") == std::string::npos) first = r;
+    for (int r = 0; r < gpus && first < 0; ++r)
+      if (!errors[r].empty()) first = r;
+    if (first >= 0) {
+      std::fprintf(stderr, "heat: rank %d error: %s\n", first, errors[first].c_str());
+      return 1;
+    }
     return 0;
   }
 

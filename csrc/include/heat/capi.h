@@ -100,6 +100,8 @@ int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double*
 /* Loopback transport: ranks are threads of this process sharing one hub. */
 int heat_loopback_hub_create(int world, void** out);
 int heat_loopback_hub_destroy(void* hub);
+/* A rank of the hub failed: peers blocked in an exchange or collective throw. */
+int heat_loopback_hub_fail(void* hub);
 int heat_solver_reset(heat_solver* s);
 int heat_solver_info(heat_solver* s, heat_block_info* out);
 int heat_solver_step(heat_solver* s, int64_t* out);

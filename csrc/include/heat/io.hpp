@@ -33,7 +33,7 @@ struct BinHeader {
   int64_t nx, ny;
   int64_t step;        // completed steps
   float cx, cy;
-  uint64_t reserved[3];
+  uint64_t reserved[3];  // [0]: bin_config_tag of the writer (0 = unknown)
 };
 static_assert(sizeof(BinHeader) == 72, "BinHeader layout");
 
@@ -44,6 +44,12 @@ void bin_create(const std::string& path, const BinHeader& h);
 void bin_write_block(const std::string& path, int64_t nx, int64_t ny, int64_t ox, int64_t oy,
                      int64_t lx, int64_t ly, const float* src, int64_t src_pitch);
 BinHeader bin_read_header(const std::string& path);
+// fsync `tmp` and rename it over `path` (atomic replacement of a checkpoint).
+void bin_commit(const std::string& tmp, const std::string& path);
+// Header tag of the modes that change the continuation of a run.
+inline uint64_t bin_config_tag(int compat, int numerics) {
+  return (uint64_t(1) << 63) | (uint64_t(numerics & 0xff) << 8) | uint64_t(compat & 0xff);
+}
 void bin_read_block(const std::string& path, int64_t ox, int64_t oy, int64_t lx, int64_t ly,
                     float* dst, int64_t dst_pitch);
 

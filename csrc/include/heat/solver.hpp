@@ -19,13 +19,18 @@
 //     boundary-first.  Measured slower on MI355X at the strong-scaling shapes
 //     (see params.hpp), kept selectable and tested.
 //   * Segments between convergence checks are captured once into a hipGraph
-//     per (length, parity) and replayed.
+//     per (length, parity, ghost state) and replayed; with a host-memory
+//     transport (ranks sharing a GPU) the exchange is a host node.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <string>
 #include <tuple>
 #include <utility>
 #include <vector>
@@ -164,6 +169,20 @@ class Solver {
   };
   std::map<std::tuple<int64_t, bool, int, int64_t, int64_t>, GraphEntry> graphs_;
   bool capturing_ = false;
+
+  // Host-staged exchanges captured into graphs (host nodes): the arguments
+  // live as long as the graphs; an error on HIP's callback thread is stored
+  // and raised by run() after the next synchronisation.
+  struct StagedCall {
+    Solver* self = nullptr;
+    std::vector<Msg> msgs;
+  };
+  static void staged_host_fn(void* p);
+  void check_staged();
+  std::deque<StagedCall> staged_calls_;
+  std::mutex staged_mu_;
+  std::atomic<bool> staged_failed_{false};
+  std::string staged_error_;
 
   // Phase timing (eager runs only).
   enum Phase { kExchange = 0, kCompute = 1, kReduce = 2 };

@@ -87,6 +87,9 @@ std::unique_ptr<Transport> make_tcp_transport(int rank, int world, const std::st
 struct LoopbackHub;
 LoopbackHub* loopback_hub_create(int world);
 void loopback_hub_destroy(LoopbackHub* hub);
+// Marks the hub failed: every rank blocked in (or later entering) a loopback
+// exchange or collective throws instead of waiting for the failed rank.
+void loopback_hub_fail(LoopbackHub* hub);
 std::unique_ptr<Transport> make_loopback_transport(LoopbackHub* hub, int rank, int device);
 
 // Callback transport (C ABI so foreign runtimes can implement it).

@@ -161,6 +161,10 @@ int heat_loopback_hub_destroy(void* hub) {
   return guard([&] { heat::loopback_hub_destroy(static_cast<heat::LoopbackHub*>(hub)); });
 }
 
+int heat_loopback_hub_fail(void* hub) {
+  return guard([&] { heat::loopback_hub_fail(static_cast<heat::LoopbackHub*>(hub)); });
+}
+
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out) {
   return guard([&] {
     heat::Params P = heat::params_from_c(p);

@@ -115,6 +115,18 @@ void bin_write_block(const std::string& path, int64_t nx, int64_t ny, int64_t ox
   ::close(fd);
 }
 
+void bin_commit(const std::string& tmp, const std::string& path) {
+  // Every rank's pwrite has returned (the caller's barrier): on one node
+  // their pages are in this file's page cache, so one fsync covers them.
+  int fd = ::open(tmp.c_str(), O_RDONLY);
+  HEAT_CHECK(fd >= 0, "cannot open %s", tmp.c_str());
+  const int rc = ::fsync(fd);
+  ::close(fd);
+  HEAT_CHECK(rc == 0, "fsync %s", tmp.c_str());
+  HEAT_CHECK(::rename(tmp.c_str(), path.c_str()) == 0, "rename %s -> %s", tmp.c_str(),
+             path.c_str());
+}
+
 BinHeader bin_read_header(const std::string& path) {
   BinHeader h{};
   int fd = ::open(path.c_str(), O_RDONLY);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -162,6 +163,7 @@ void Solver::free_all() {
     if (s_comm_) (void)hipStreamSynchronize(s_comm_);
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second.exec);
     graphs_.clear();
+    staged_calls_.clear();
     for (auto& b : base_)
       if (b) (void)hipFree(b);
     for (auto& b : ew_)
@@ -284,8 +286,20 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
         HIP_CHECK(hipMemcpyAsync(stage_send_[i], msgs[i].sbuf, msgs[i].sbytes,
                                  hipMemcpyDeviceToHost, st));
     }
-    HIP_CHECK(hipStreamSynchronize(st));
-    tr_->sendrecv(host.data(), int(host.size()), st);
+    if (capturing_) {
+      // Inside a graph the host-side transfer becomes a host node: HIP runs
+      // it on its callback thread, in stream order between the staging
+      // copies, every time the graph replays.  This is how the multi-rank
+      // graph path (segment graphs keyed by ghost state, deep halos) runs
+      // with several processes on ONE GPU, where RCCL refuses two ranks.
+      StagedCall& c = staged_calls_.emplace_back();
+      c.self = this;
+      c.msgs = std::move(host);
+      HIP_CHECK(hipLaunchHostFunc(st, &Solver::staged_host_fn, &c));
+    } else {
+      HIP_CHECK(hipStreamSynchronize(st));
+      tr_->sendrecv(host.data(), int(host.size()), st);
+    }
     for (size_t i = 0; i < msgs.size(); ++i)
       if (msgs[i].rbytes)
         HIP_CHECK(hipMemcpyAsync(msgs[i].rbuf, stage_recv_[i], msgs[i].rbytes,
@@ -331,6 +345,25 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
     do_sendrecv(msgs);
   }
   ++stat_exchanges_;
+}
+
+void Solver::staged_host_fn(void* p) {
+  auto* c = static_cast<StagedCall*>(p);
+  Solver* self = c->self;
+  if (self->staged_failed_.load()) return;  // a failed transport: skip, reported by run()
+  try {
+    self->tr_->sendrecv(c->msgs.data(), int(c->msgs.size()), nullptr);
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> lk(self->staged_mu_);
+    self->staged_error_ = e.what();
+    self->staged_failed_.store(true);
+  }
+}
+
+void Solver::check_staged() {
+  if (!staged_failed_.load()) return;
+  std::lock_guard<std::mutex> lk(staged_mu_);
+  throw_error(__FILE__, __LINE__, "host-staged exchange in a graph failed: " + staged_error_);
 }
 
 // ---------------------------------------------------------------------------
@@ -536,6 +569,7 @@ float Solver::finish_resid() {
   float r;
   if (on_gpu()) {
     HIP_CHECK(hipStreamSynchronize(s_comp_));
+    check_staged();
     tr_->check();
     std::memcpy(&r, h_resid_, 4);
     if (!tr_->device_memory()) tr_->allreduce_max(&r, 1, nullptr);
@@ -618,15 +652,16 @@ RunStats Solver::run(int64_t steps) {
   synchronize();
   const double t0 = now_s();
   const bool gpu = on_gpu();
-  const bool can_graph = gpu && P_.use_graph && !staged_ && !timing_ &&
-                         (tr_->world() == 1 || tr_->graph_capturable()) &&
+  // Staged (host-memory) transports are captured as host nodes.
+  const bool can_graph = gpu && P_.use_graph && !timing_ &&
+                         (tr_->world() == 1 || tr_->graph_capturable() || staged_) &&
                          env_int("HEAT_GRAPH", 1) != 0;
   if (timing_) {
     spans_.clear();
     pool_used_ = 0;
     phase_acc_[0] = phase_acc_[1] = phase_acc_[2] = 0.0;
   }
-  if (can_graph && tr_->world() > 1 && !warmed_) {
+  if (can_graph && tr_->world() > 1 && tr_->device_memory() && !warmed_) {
     // Let RCCL establish its connections outside of stream capture.  A halo
     // exchange of the current buffer is idempotent.
     exchange(cur_, H_, s_comp_);
@@ -710,6 +745,7 @@ RunStats Solver::run(int64_t steps) {
     }
   }
   synchronize();
+  check_staged();
   tr_->check();
   s.seconds = now_s() - t0;
   if (timing_) {
@@ -922,6 +958,10 @@ Checksum Solver::checksum() {
 }
 
 void Solver::write_bin(const std::string& path) {
+  // Written as `path`.tmp by every rank, then renamed by rank 0 once all
+  // blocks are in: a crash mid-write (a --checkpoint-every run) leaves the
+  // previous checkpoint intact.
+  const std::string tmp = path + ".tmp";
   if (tr_->rank() == 0) {
     BinHeader h{};
     std::memcpy(h.magic, "HEATF32", 8);
@@ -932,12 +972,15 @@ void Solver::write_bin(const std::string& path) {
     h.step = step_;
     h.cx = P_.cx;
     h.cy = P_.cy;
-    bin_create(path, h);
+    h.reserved[0] = bin_config_tag(int(P_.compat), int(P_.numerics));
+    bin_create(tmp, h);
   }
   tr_->barrier();
   std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
   copy_owned(mine.data(), blk_.ly);
-  bin_write_block(path, P_.nx, P_.ny, blk_.ox, blk_.oy, blk_.lx, blk_.ly, mine.data(), blk_.ly);
+  bin_write_block(tmp, P_.nx, P_.ny, blk_.ox, blk_.oy, blk_.lx, blk_.ly, mine.data(), blk_.ly);
+  tr_->barrier();
+  if (tr_->rank() == 0) bin_commit(tmp, path);
   tr_->barrier();
 }
 
@@ -945,6 +988,19 @@ void Solver::read_bin(const std::string& path) {
   BinHeader h = bin_read_header(path);
   HEAT_CHECK(h.nx == P_.nx && h.ny == P_.ny, "checkpoint is %lldx%lld, run is %lldx%lld",
              (long long)h.nx, (long long)h.ny, (long long)P_.nx, (long long)P_.ny);
+  // A checkpoint of a different physics or compat mode still loads (the
+  // state is just a grid), but the continuation is not the run it came from.
+  if (tr_->rank() == 0) {
+    if (h.cx != P_.cx || h.cy != P_.cy)
+      std::fprintf(stderr, "heat: warning: %s was written with cx=%g cy=%g, this run uses "
+                   "cx=%g cy=%g\n", path.c_str(), double(h.cx), double(h.cy), double(P_.cx),
+                   double(P_.cy));
+    const uint64_t tag = bin_config_tag(int(P_.compat), int(P_.numerics));
+    if (h.reserved[0] != 0 && h.reserved[0] != tag)
+      std::fprintf(stderr, "heat: warning: %s was written under another --compat/--numerics "
+                   "mode (tag %llx, this run %llx)\n", path.c_str(),
+                   (unsigned long long)h.reserved[0], (unsigned long long)tag);
+  }
   std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
   bin_read_block(path, blk_.ox, blk_.oy, blk_.lx, blk_.ly, mine.data(), blk_.ly);
   load_owned(mine.data(), blk_.ly, h.step);

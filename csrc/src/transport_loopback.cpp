@@ -51,6 +51,9 @@ struct LoopbackHub {
     }
   };
   const int world;
+  // Set when a rank fails (loopback_hub_fail): every blocked or later wait
+  // throws instead of waiting forever for a peer that will never post.
+  bool failed = false;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<std::deque<std::shared_ptr<Post>>> box;  // [src * world + dst]
@@ -74,8 +77,15 @@ struct LoopbackHub {
       ++generation;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return generation != gen; });
+      wait(lk, [&] { return generation != gen; });
     }
+  }
+
+  // cv.wait that gives up once a peer rank has failed.
+  template <class Pred>
+  void wait(std::unique_lock<std::mutex>& lk, Pred pred) {
+    cv.wait(lk, [&] { return failed || pred(); });
+    if (!pred()) throw_error(__FILE__, __LINE__, "loopback: a peer rank failed");
   }
 };
 
@@ -116,7 +126,7 @@ class LoopbackTransport final : public Transport {
       {
         std::unique_lock<std::mutex> lk(hub_->mu);
         auto& q = hub_->box[size_t(msgs[i].peer) * hub_->world + rank_];
-        hub_->cv.wait(lk, [&] { return !q.empty(); });
+        hub_->wait(lk, [&] { return !q.empty(); });
         p = q.front();
         q.pop_front();
       }
@@ -138,7 +148,7 @@ class LoopbackTransport final : public Transport {
     for (auto& p : mine) {
       {
         std::unique_lock<std::mutex> lk(hub_->mu);
-        hub_->cv.wait(lk, [&] { return p->done; });
+        hub_->wait(lk, [&] { return p->done; });
       }
       HIP_CHECK(hipStreamWaitEvent(st, p->consumed, 0));
     }
@@ -226,6 +236,13 @@ LoopbackHub* loopback_hub_create(int world) {
   return new LoopbackHub(world);
 }
 void loopback_hub_destroy(LoopbackHub* hub) { delete hub; }
+void loopback_hub_fail(LoopbackHub* hub) {
+  {
+    std::lock_guard<std::mutex> lk(hub->mu);
+    hub->failed = true;
+  }
+  hub->cv.notify_all();
+}
 
 std::unique_ptr<Transport> make_loopback_transport(LoopbackHub* hub, int rank, int device) {
   return std::make_unique<LoopbackTransport>(hub, rank, device);

@@ -114,6 +114,7 @@ _SIGS = {
     "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
     "heat_rccl_self_test": (c_int, [c_int, c_int64, c_int, c_int, POINTER(c_double)]),
     "heat_loopback_hub_destroy": (c_int, [c_void_p]),
+    "heat_loopback_hub_fail": (c_int, [c_void_p]),
     "heat_solver_reset": (c_int, [c_void_p]),
     "heat_solver_info": (c_int, [c_void_p, POINTER(HeatBlockInfo)]),
     "heat_solver_step": (c_int, [c_void_p, POINTER(c_int64)]),

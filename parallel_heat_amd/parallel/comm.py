@@ -160,6 +160,11 @@ class LoopbackHub:
         self.world = world
         self.handle = h
 
+    def fail(self) -> None:
+        """A rank failed: its peers' pending and future exchanges raise."""
+        if self.handle:
+            _native.call("heat_loopback_hub_fail", self.handle)
+
     def close(self) -> None:
         if self.handle:
             _native.call("heat_loopback_hub_destroy", self.handle)

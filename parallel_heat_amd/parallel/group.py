@@ -41,6 +41,9 @@ def run_group(config: HeatConfig, world: int, fn: Callable[[HeatSolver], object]
                 results[rank] = fn(s)
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             errors[rank] = e
+            # Unblock the peers (they would wait forever for this rank's
+            # messages); they raise "a peer rank failed" in turn.
+            hub.fail()
 
     threads = [threading.Thread(target=body, args=(r,), name=f"heat-rank{r}")
                for r in range(world)]
@@ -49,7 +52,10 @@ def run_group(config: HeatConfig, world: int, fn: Callable[[HeatSolver], object]
     for t in threads:
         t.join()
     hub.close()
-    for r, e in enumerate(errors):
-        if e is not None:
-            raise RuntimeError(f"rank {r} failed: {e}") from e
+    # Report the first failure, not the peers' "a peer rank failed" echoes.
+    failed = [(r, e) for r, e in enumerate(errors) if e is not None]
+    if failed:
+        own = [(r, e) for r, e in failed if "a peer rank failed" not in str(e)]
+        r, e = (own or failed)[0]
+        raise RuntimeError(f"rank {r} failed: {e}") from e
     return results

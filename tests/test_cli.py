@@ -105,6 +105,18 @@ def test_cli_checkpoint_resume(tmp_path):
     assert hb["step"] == 40 and hc["step"] == 40
     assert np.array_equal(np.asarray(a), np.asarray(b))
     assert np.array_equal(np.asarray(a), np.asarray(c))
+    # written as ck.bin.tmp and renamed: no temporary left behind
+    assert not (tmp_path / "ck.bin.tmp").exists()
+
+
+def test_cli_resume_warns_on_other_physics(tmp_path):
+    heat(["--backend", "cpu", "--nx", "16", "--ny", "16", "--steps", "5", "--init", "random",
+          "--out", "s5.bin", "--out-format", "bin"], tmp_path)
+    p = subprocess.run([HEAT, "--backend", "cpu", "--nx", "16", "--ny", "16", "--steps", "8",
+                        "--cx", "0.2", "--resume", "s5.bin", "--out", "none"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert "warning" in p.stderr and "cx=0.1" in p.stderr
 
 
 def test_python_cli(tmp_path):

@@ -3,7 +3,13 @@ through host-staged torch.distributed (gloo).  This runs the real GPU kernels,
 pack/unpack and all three pass schedules (sync deep-halo, exchange-first
 overlap, boundary-first pipeline, the overlap ones with the comm stream
 running concurrently with the interior kernel) under a real decomposition;
-results must equal the single-rank GPU run bit for bit."""
+results must equal the single-rank GPU run bit for bit.
+
+By default these runs capture their segments into hipGraphs with the staged
+exchange as a host node, i.e. the multi-rank graph path RCCL runs take
+(graphs keyed by segment length, parity and ghost state; deep halos carried
+across replays) runs here with world > 1; `use_graph=False` keeps the eager
+path covered."""
 import numpy as np
 import pytest
 
@@ -59,3 +65,29 @@ def test_gpu_distributed_convergence(gpu, tmp_path, schedule, decomp):
     assert bool(res["conv"]) == r.converged
     assert int(res["conv_at"]) == r.converged_at and int(res["done"]) == r.steps_done
     assert np.array_equal(res["grid"], ref)
+
+
+@pytest.mark.parametrize("world,kw", [(2, dict(decomp="rows", schedule="sync")),
+                                      (4, dict(decomp="auto", schedule="pipeline"))])
+def test_gpu_ranks_one_device_eager(gpu, tmp_path, world, kw):
+    base = {**BASE, **kw, "use_graph": False}
+    res = run_world(world, base, 45, tmp_path, transport="torch")
+    ref, _ = single(base, 45)
+    assert np.array_equal(res["grid"], ref)
+
+
+@pytest.mark.parametrize("converge", [False, True])
+def test_gpu_graph_replay_bench_shape(gpu, tmp_path, converge):
+    # bench.py's shape in miniature: rows slabs, auto depth and halo, runs of
+    # one "step" (100 iterations) replayed several times from cached graphs,
+    # with and without the residual all-reduce of the convergence check.
+    base = dict(nx=512, ny=384, steps=0, init="random", seed=1234, backend="hip",
+                decomp="rows", converge=converge, check_interval=50, eps=1e-12)
+    res = run_world(2, base, 0, tmp_path, transport="torch", chunks=[100] * 5)
+    with HeatSolver(HeatConfig(**{**base, "decomp": "auto"})) as s:
+        for _ in range(5):
+            s.run(100)
+        ref, h = s.gather(), s.checksum()["hash"]
+    assert int(res["done"]) == 500
+    assert np.array_equal(res["grid"], ref)
+    assert str(res["hash"]) == h

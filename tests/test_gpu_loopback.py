@@ -158,3 +158,19 @@ def test_loopback_mfma_kernel_invariance(gpu):
     assert np.array_equal(next(g for g in res if g is not None), want)
     ref, _, _ = single(cfg.replace(kernel="tb", tb_depth=8), 21)
     assert np.abs(want - ref).max() <= 1e-3
+
+
+def test_loopback_failed_rank_unblocks_peers(gpu):
+    # Rank 1 dies before its first exchange; rank 0 would wait forever for
+    # its halo rows.  The hub is marked failed, rank 0 raises, and run_group
+    # reports rank 1's own error.
+    cfg = HeatConfig(**{**BASE, "decomp": "rows"})
+
+    def fn(s):
+        if s.rank == 1:
+            raise ValueError("injected failure on rank 1")
+        s.run(45)
+        return s.gather()
+
+    with pytest.raises(RuntimeError, match="rank 1 failed: injected failure"):
+        run_group(cfg, 2, fn)
