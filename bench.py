@@ -25,6 +25,12 @@ benchmarked (multi-GPU, graph-captured, temporally blocked) run computed
 exactly the reference field.  A mismatch prints `"verified": false` and exits
 non-zero.
 
+Multi-GPU autotune (`--no-autotune` skips it): before the warmup, every
+decomposition candidate (rows slabs, the 2-D MPI_Dims_create grid) x pass
+schedule is timed for two steps on the real ranks (max over ranks) and the
+fastest is benchmarked; the table is in the JSON line ("autotune") and the
+choice in config.parallelism.
+
 Failure handling: RCCL must come up on every rank (the ranks agree through
 torch.distributed before going on); if it fails anywhere the run exits
 non-zero, unless `--allow-fallback` lets ALL ranks switch together to halos
@@ -78,6 +84,11 @@ def main() -> int:
                     help="skip the post-run check against a single-rank LDS-kernel run")
     ap.add_argument("--allow-fallback", action="store_true",
                     help="if RCCL fails on every rank, run with host-staged halos over gloo")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="multi-GPU: skip timing the decomposition/schedule candidates "
+                         "(use --decomp/--schedule as given)")
+    ap.add_argument("--autotune-schedules", default="sync",
+                    help="comma list of pass schedules the multi-GPU autotune tries")
     ap.add_argument("--watchdog-s", type=float, default=900.0,
                     help="abort (stack dump, exit 1) if one phase takes longer than this")
     args = ap.parse_args()
@@ -120,6 +131,23 @@ def main() -> int:
                      schedule=args.schedule, halo_passes=args.halo_passes,
                      phase_timing=args.phase_timing)
     info = DistInfo(rank, world, local_rank)
+
+    tuning = None
+    if world > 1 and not args.no_autotune:
+        # The fastest decomposition (rows slabs vs the 2-D dims_create grid)
+        # and pass schedule depend on xGMI link bandwidth and the per-rank
+        # block shape: time each on the real ranks before the timed region.
+        from parallel_heat_amd.parallel.tune import autotune, default_candidates
+
+        watchdog("autotune", args.watchdog_s)
+        cands = default_candidates(cfg, world,
+                                   schedules=[x for x in args.autotune_schedules.split(",") if x])
+        try:
+            cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=2,
+                                   log=(lambda m: log(rank, m)) if args.verbose else None)
+        except _native.NativeError as e:
+            # e.g. RCCL unavailable: the transport vote below decides.
+            log(rank, f"autotune failed ({e}); using --decomp {args.decomp}")
 
     solver = None
     try:
@@ -209,6 +237,8 @@ def main() -> int:
             },
             "verified": verified,
         }
+        if tuning is not None:
+            line["autotune"] = tuning
         if check:
             line["verification"] = check
         if args.verbose:

@@ -61,3 +61,49 @@ def run_world(world, cfg_kwargs, steps, tmp_path, transport="torch", chunks=None
     mp.spawn(worker, args=(world, free_port(), cfg_kwargs, steps, out, transport, chunks),
              nprocs=world, join=True)
     return dict(np.load(out))
+
+
+def tune_worker(rank, world, port, cfg_kwargs, out_path, transport):
+    """Runs parallel.tune.autotune on every rank; rank 0 saves the choice."""
+    import json
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parallel_heat_amd import HeatConfig
+    from parallel_heat_amd.parallel.comm import DistInfo
+    from parallel_heat_amd.parallel.tune import autotune, default_candidates
+
+    cfg = HeatConfig(**cfg_kwargs)
+    cands = default_candidates(cfg, world, schedules=["sync", "overlap"], halo_passes=[0, 2])
+    info = DistInfo(rank, world, rank)
+    make = None
+    if transport != "auto":  # e.g. GPU ranks sharing one device: host-staged halos
+        from parallel_heat_amd import HeatSolver
+
+        def make(c):
+            return HeatSolver(c, transport=transport, dist_info=info,
+                              device=0 if c.backend == "hip" else None)
+    best, table = autotune(cfg, info, cands, steps=20, repeats=1, make=make)
+    choice = [best.decomp, best.schedule, best.halo_passes]
+    got = [None] * world
+    dist.all_gather_object(got, choice)
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"choices": got, "table": table}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_tune(world, cfg_kwargs, tmp_path, transport="auto"):
+    import json
+
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / f"tune_{world}_{os.getpid()}.json")
+    mp.spawn(tune_worker, args=(world, free_port(), cfg_kwargs, out, transport), nprocs=world,
+             join=True)
+    with open(out) as f:
+        return json.load(f)

@@ -95,3 +95,18 @@ def test_scatter_then_run_distributed(tmp_path):
     res = run_world(3, kw, 12, tmp_path)
     ref, _ = single(dict(nx=31, ny=27, steps=0, init="random", seed=77, backend="cpu"), 12)
     assert np.array_equal(res["grid"], ref)
+
+
+def test_autotune_collective_gloo(tmp_path):
+    # Four ranks time rows slabs vs the 2x2 grid x {sync (m default, m=2),
+    # overlap}; every rank must come out with the same choice, and the
+    # table must list every candidate with a time.
+    from .dist_worker import run_tune
+
+    res = run_tune(4, dict(nx=64, ny=64, steps=0, init="random", seed=3, backend="cpu",
+                           tb_depth=2), tmp_path)
+    assert all(c == res["choices"][0] for c in res["choices"])
+    layouts = {(r["px"], r["py"]) for r in res["table"]}
+    assert layouts == {(4, 1), (2, 2)}
+    assert len(res["table"]) == 6
+    assert all(r["ms_per_1000_iters"] > 0 for r in res["table"])

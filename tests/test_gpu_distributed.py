@@ -91,3 +91,16 @@ def test_gpu_graph_replay_bench_shape(gpu, tmp_path, converge):
     assert int(res["done"]) == 500
     assert np.array_equal(res["grid"], ref)
     assert str(res["hash"]) == h
+
+
+def test_gpu_autotune_staged(gpu, tmp_path):
+    # The multi-GPU autotune of bench.py, with two GPU ranks sharing cuda:0
+    # (host-staged halos in captured graphs instead of RCCL).
+    from .dist_worker import run_tune
+
+    res = run_tune(2, dict(nx=256, ny=512, steps=0, init="random", seed=3, backend="hip"),
+                   tmp_path, transport="torch")
+    assert res["choices"][0] == res["choices"][1]
+    assert {(r["px"], r["py"]) for r in res["table"]} == {(2, 1), (1, 2)} or \
+        {(r["px"], r["py"]) for r in res["table"]} == {(2, 1)}
+    assert all("ms_per_1000_iters" in r for r in res["table"])

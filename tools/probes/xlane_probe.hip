@@ -12,6 +12,12 @@
 //   4  west: row_bcast:15 + row_shr:1, east: ds_bpermute
 //   5  both ds_bpermute (the level-split kernel's form)
 //   6  west: row_bcast:15 + row_shr:1, east: row_shl:1 over a permlane-fixed copy
+//   7  both ds_bpermute, issued one iteration early: the shifts of a level's
+//      new row are posted right after the next level has consumed the
+//      previous ones, so their LDS latency hides behind a whole iteration
+//      (compiler-scheduled: it sinks them back next to their uses)
+//   8  as 7 with the ds_bpermute issued and waited for in inline asm, so the
+//      early issue survives scheduling (waits: lgkmcnt(2K-2), in-order LDS)
 // and prints cycles per float4 row update at the nominal clock for 1..4 waves
 // per SIMD, plus a correctness flag of the shift formula of each mode.
 #include <hip/hip_runtime.h>
@@ -102,6 +108,16 @@ __device__ __forceinline__ f4 upd(const f4& a, const f4& b, const f4& c, float c
   return r;
 }
 
+__device__ __forceinline__ f4 upd_pre(const f4& a, const f4& b, const f4& c, float w, float e,
+                                      float cx, float cy) {
+  f4 r;
+  r.x = st(b.x, a.x, c.x, w, b.y, cx, cy);
+  r.y = st(b.y, a.y, c.y, b.x, b.z, cx, cy);
+  r.z = st(b.z, a.z, c.z, b.y, b.w, cx, cy);
+  r.w = st(b.w, a.w, c.w, e, b.z, cx, cy);
+  return r;
+}
+
 template <int K, int MODE>
 __global__ __launch_bounds__(256) void chain(float* out, int iters, float cx, float cy) {
   f4 R[K][3];
@@ -110,6 +126,71 @@ __global__ __launch_bounds__(256) void chain(float* out, int iters, float cx, fl
   for (int s = 0; s < K; ++s)
 #pragma unroll
     for (int j = 0; j < 3; ++j) R[s][j] = f4(float(s + j));
+  if constexpr (MODE == 8) {
+    // Same schedule as MODE 7; each shifted value is produced by an asm
+    // ds_bpermute (opaque to the compiler's waitcnt pass) and read only
+    // through an asm s_waitcnt that takes it as an in/out operand, so no
+    // use can move above the wait.  2K bpermutes are in flight per
+    // iteration; a value is consumed one iteration after issue, when the
+    // 2K-2 bpermutes issued after it may still be pending.
+    float ws[K], es[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) ws[s] = es[s] = float(s);
+    const int l = threadIdx.x & 63;
+    const int aw = ((l + 63) & 63) << 2, ae = ((l + 1) & 63) << 2;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int U = 0; U < 3; ++U) {
+        R[0][U] = in;
+#pragma unroll
+        for (int s = 1; s <= K; ++s) {
+          float w = ws[s - 1], e = es[s - 1];
+          // the two shifts of level s-1 were issued 2K-2 LDS ops ago at least
+          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(w), "+v"(e) : "n"(2 * K - 2 > 15 ? 15 : 2 * K - 2));
+          f4 r = upd_pre(R[s - 1][(U - s - 1 + 30) % 3], R[s - 1][(U - s + 30) % 3],
+                         R[s - 1][(U - s + 1 + 30) % 3], w, e, cx, cy);
+          if (s < K) R[s][(U - s + 30) % 3] = r; else in = r;
+          const f4& nw = R[s - 1][(U - s + 1 + 30) % 3];
+          asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(ws[s - 1]) : "v"(aw), "v"(nw.w));
+          asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(es[s - 1]) : "v"(ae), "v"(nw.x));
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float s = in.x + in.y + in.z + in.w + ws[0] + es[0];
+    if (s == 1234.5f) out[threadIdx.x] = s;
+    return;
+  }
+  if constexpr (MODE == 7) {
+    // ws[s]/es[s]: lane shifts of level s's newest row, consumed by level s+1
+    // in the next iteration (level s's row i-s is level s+1's centre row then).
+    float ws[K], es[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) ws[s] = es[s] = float(s);
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int U = 0; U < 3; ++U) {
+        R[0][U] = in;
+#pragma unroll
+        for (int s = 1; s < K; ++s) {
+          R[s][(U - s + 30) % 3] = upd_pre(R[s - 1][(U - s - 1 + 30) % 3], R[s - 1][(U - s + 30) % 3],
+                                           R[s - 1][(U - s + 1 + 30) % 3], ws[s - 1], es[s - 1], cx, cy);
+          // level s-1's newest row (row i-s+1) is the centre of level s next time
+          const f4& nw = R[s - 1][(U - s + 1 + 30) % 3];
+          ws[s - 1] = west<5>(nw.w);
+          es[s - 1] = east<5>(nw.x);
+        }
+        in = upd_pre(R[K - 1][(U - K - 1 + 30) % 3], R[K - 1][(U - K + 30) % 3],
+                     R[K - 1][(U - K + 1 + 30) % 3], ws[K - 1], es[K - 1], cx, cy);
+        const f4& nw = R[K - 1][(U - K + 1 + 30) % 3];
+        ws[K - 1] = west<5>(nw.w);
+        es[K - 1] = east<5>(nw.x);
+      }
+    }
+    const float s = in.x + in.y + in.z + in.w;
+    if (s == 1234.5f) out[threadIdx.x] = s;
+    return;
+  }
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int U = 0; U < 3; ++U) {
@@ -206,9 +287,16 @@ int main() {
   run<8, 4>(cus, clk, out);
   run<8, 5>(cus, clk, out);
   run<8, 6>(cus, clk, out);
+  run<8, 7>(cus, clk, out);
+  run<8, 8>(cus, clk, out);
+  run<6, 8>(cus, clk, out);
+  run<12, 8>(cus, clk, out);
+  run<4, 7>(cus, clk, out);
+  run<6, 7>(cus, clk, out);
   run<12, 0>(cus, clk, out);
-  run<12, 2>(cus, clk, out);
-  run<12, 3>(cus, clk, out);
+  run<12, 1>(cus, clk, out);
+  run<12, 5>(cus, clk, out);
+  run<12, 7>(cus, clk, out);
   CHECK(hipFree(out));
   return 0;
 }
