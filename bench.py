@@ -118,6 +118,13 @@ def main() -> int:
     torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if os.environ.get("HEAT_RCCL_HOST_PER_RANK") == "1":
+            # Rehearsal hook for a 1-GPU box (tools/rccl_rehearsal.sh): RCCL
+            # refuses two ranks on one device of one host, so each rank claims
+            # its own host id and the ranks talk over RCCL's socket transport.
+            # The API path (grouped send/recv captured in hipGraphs, the
+            # all-reduces, torch's own nccl group) is the one a real node runs.
+            os.environ["NCCL_HOSTID"] = f"heat-rank-{rank}"
         dist.init_process_group("nccl")
 
     from parallel_heat_amd import HeatConfig, HeatSolver, _native

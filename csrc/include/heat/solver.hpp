@@ -119,8 +119,9 @@ class Solver {
   void enqueue_segment(int64_t n, bool resid);
   void enqueue_pass(int k, bool resid);
   void exchange(int buf, int k, hipStream_t st);
+  // `st`: the stream to launch on (nullptr = the compute stream).
   void compute_gpu(int k, bool resid, bool split, int part, int band = 0, int64_t er = 0,
-                   int64_t ec = 0);
+                   int64_t ec = 0, hipStream_t st = nullptr);
   void compute_cpu(int k, bool resid, int64_t er, int64_t ec);
   std::pair<int64_t, int64_t> ensure_ghosts(int k, hipStream_t st);
   float finish_resid();

@@ -370,8 +370,9 @@ void Solver::check_staged() {
 // compute
 // ---------------------------------------------------------------------------
 void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int64_t er,
-                         int64_t ec) {
-  PhaseScope phase(this, kCompute, s_comp_);
+                         int64_t ec, hipStream_t st) {
+  if (!st) st = s_comp_;
+  PhaseScope phase(this, kCompute, st);
   const float* src = field_[cur_];
   float* dst = field_[cur_ ^ 1];
   gpu::StencilGeom g;
@@ -401,18 +402,18 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
       const float* a = field_[cur_];
       float* d = field_[cur_ ^ 1];
       if (P_.kernel == KernelKind::Lds)
-        gpu::lds_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+        gpu::lds_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
       else if (P_.kernel == KernelKind::Mfma)
-        gpu::mfma_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+        gpu::mfma_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
       else
-        gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, s_comp_);
+        gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
       cur_ ^= 1;
     }
     return;
   }
 
   if (!split) {
-    gpu::tb_step(src, dst, g, &own, 1, k, r, s_comp_, waves_target);
+    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target);
     return;
   }
   // Boundary bands are `band` >= k deep (k for exchange-first; H for the
@@ -424,10 +425,10 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
   const int64_t c1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
   if (part == 0) {
     Box in{r0, r1, c0, c1};
-    gpu::tb_step(src, dst, g, &in, 1, k, r, s_comp_, waves_target);
+    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target);
   } else {
     Box b[4] = {{0, r0, 0, ly}, {r1, lx, 0, ly}, {r0, r1, 0, c0}, {r0, r1, c1, ly}};
-    gpu::tb_step(src, dst, g, b, 4, k, r, s_comp_, waves_target);
+    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target);
     // cur_ flips once per pass, after the boundary part.
   }
 }
@@ -488,33 +489,51 @@ void Solver::enqueue_pass(int k, bool resid) {
     const int64_t ic0 = nb[West] >= 0 ? round_up(band, 4) : 0;
     const int64_t ic1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
     const bool interior_ok = ir1 > ir0 && ic1 > ic0;
+    // Which work goes on the side stream of the overlap schedules.  Eagerly
+    // the exchange does (the high-priority comm stream, so RCCL's kernels
+    // are dispatched ahead of queued stencil workgroups).  Under capture a
+    // device transport keeps its collectives on the capture's origin stream
+    // and the interior kernel forks instead: RCCL called on a forked
+    // capturing stream crashes inside the library (RCCL 2.26, measured with
+    // tools/rccl_mr_diag.sh), and a graph has the same dependency DAG either
+    // way (exchange || interior, then the bands).
+    const bool comm_on_side = !(capturing_ && tr_->device_memory());
     if (!multi) {
       compute_gpu(k, resid, false, 0);
     } else if (sched_ == Schedule::Pipeline) {
       // Boundary-first: the H-deep ghosts of cur_ were exchanged by the
       // previous pass (or now, if stale).  Compute the H-deep boundary bands,
       // then post the NEXT pass's exchange (its send rows/columns all lie in
-      // the bands) on the high-priority comm stream, concurrent with the
-      // interior launch.
+      // the bands) concurrent with the interior launch.
       if (gr_ < H_ || gc_ < H_) {
-        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-        exchange(cur_, H_, s_comm_);
-        HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-        comm_pending_ = true;
+        if (comm_on_side) {
+          HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+          HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+          exchange(cur_, H_, s_comm_);
+          HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+          comm_pending_ = true;
+        } else {
+          exchange(cur_, H_, s_comp_);  // the bands wait for it anyway
+        }
       }
-      // Only wait on an exchange posted in this segment: a segment ends by
+      // Only wait on side work posted in this segment: a segment ends by
       // joining the comm stream, and a captured graph may not wait on an
       // event recorded outside its capture.
       if (comm_pending_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
       compute_gpu(k, resid, true, 1, band);
       HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-      // The interior is enqueued before the exchange: the stream semantics
-      // are the same (s_comm waits for the bands only), and a host-staged
-      // exchange, which blocks the host, then overlaps the interior too.
-      compute_gpu(k, resid, true, 0, band);
-      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-      exchange(cur_ ^ 1, H_, s_comm_);
+      if (comm_on_side) {
+        // The interior is enqueued before the exchange: the stream semantics
+        // are the same (s_comm waits for the bands only), and a host-staged
+        // exchange, which blocks the host, then overlaps the interior too.
+        compute_gpu(k, resid, true, 0, band);
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+        exchange(cur_ ^ 1, H_, s_comm_);
+      } else {
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+        compute_gpu(k, resid, true, 0, band, 0, 0, s_comm_);
+        exchange(cur_ ^ 1, H_, s_comp_);
+      }
       HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
       comm_pending_ = true;
       gr_ = gc_ = H_;  // for the buffer that becomes cur_ below
@@ -522,9 +541,15 @@ void Solver::enqueue_pass(int k, bool resid) {
       // Exchange-first: exchange || interior, then the boundary bands.
       HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-      exchange(cur_, k, s_comm_);
-      HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-      compute_gpu(k, resid, true, 0);
+      if (comm_on_side) {
+        exchange(cur_, k, s_comm_);
+        HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+        compute_gpu(k, resid, true, 0);
+      } else {
+        compute_gpu(k, resid, true, 0, 0, 0, 0, s_comm_);
+        HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+        exchange(cur_, k, s_comp_);
+      }
       HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
       compute_gpu(k, resid, true, 1);
       gr_ = gc_ = 0;

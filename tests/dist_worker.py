@@ -19,11 +19,21 @@ def free_port() -> int:
     return p
 
 
+def rccl_host_per_rank(rank):
+    """Let several RCCL ranks share one GPU: each rank claims its own host id,
+    so RCCL's duplicate-device check passes and the ranks talk over its socket
+    transport on loopback (same hook as bench.py's HEAT_RCCL_HOST_PER_RANK)."""
+    os.environ.update(NCCL_HOSTID=f"heat-rank-{rank}", NCCL_SOCKET_IFNAME="lo",
+                      NCCL_IB_DISABLE="1")
+
+
 def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if transport == "rccl":
+        rccl_host_per_rank(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from parallel_heat_amd import HeatConfig, HeatSolver
     from parallel_heat_amd.parallel.comm import DistInfo
@@ -71,6 +81,8 @@ def tune_worker(rank, world, port, cfg_kwargs, out_path, transport):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if transport == "rccl":
+        rccl_host_per_rank(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from parallel_heat_amd import HeatConfig
     from parallel_heat_amd.parallel.comm import DistInfo

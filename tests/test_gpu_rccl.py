@@ -1,8 +1,7 @@
 """The RCCL transport on the real library, one rank: grouped self
 send/recv eagerly and inside a captured hipGraph (the way the solver's
-passes are replayed), plus the all-reduce.  Multi-rank RCCL needs one GPU
-per rank (RCCL refuses two ranks on one device); the same solver code path
-with a device-memory transport is covered by test_gpu_loopback.py."""
+passes are replayed), plus the all-reduce.  Multi-rank RCCL on one GPU (one
+RCCL host id per rank, socket transport) is test_gpu_rccl_multirank.py."""
 import ctypes
 
 import pytest
