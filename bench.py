@@ -27,8 +27,10 @@ non-zero.
 
 Multi-GPU autotune (`--no-autotune` skips it): before the warmup, every
 decomposition candidate (rows slabs, the 2-D MPI_Dims_create grid) x pass
-schedule is timed for two steps on the real ranks (max over ranks) and the
-fastest is benchmarked; the table is in the JSON line ("autotune") and the
+schedule (deep-halo sync with the default and a doubled exchange interval,
+boundary-first pipeline overlapping the exchange with the interior) is timed
+for two steps on the real ranks (max over ranks) and the fastest is
+benchmarked; the table is in the JSON line ("autotune") and the
 choice in config.parallelism.
 
 Failure handling: RCCL must come up on every rank (the ranks agree through
@@ -87,8 +89,10 @@ def main() -> int:
     ap.add_argument("--no-autotune", action="store_true",
                     help="multi-GPU: skip timing the decomposition/schedule candidates "
                          "(use --decomp/--schedule as given)")
-    ap.add_argument("--autotune-schedules", default="sync",
+    ap.add_argument("--autotune-schedules", default="sync,pipeline",
                     help="comma list of pass schedules the multi-GPU autotune tries")
+    ap.add_argument("--autotune-halo-passes", default="0,16",
+                    help="comma list of sync-schedule passes per exchange (0 = engine default)")
     ap.add_argument("--watchdog-s", type=float, default=900.0,
                     help="abort (stack dump, exit 1) if one phase takes longer than this")
     args = ap.parse_args()
@@ -148,7 +152,9 @@ def main() -> int:
 
         watchdog("autotune", args.watchdog_s)
         cands = default_candidates(cfg, world,
-                                   schedules=[x for x in args.autotune_schedules.split(",") if x])
+                                   schedules=[x for x in args.autotune_schedules.split(",") if x],
+                                   halo_passes=[int(x) for x in
+                                                args.autotune_halo_passes.split(",") if x])
         try:
             cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=2,
                                    log=(lambda m: log(rank, m)) if args.verbose else None)
