@@ -12,7 +12,7 @@ CXXSTD  := -std=c++17
 # Host code: x86-64-v3 (FMA/AVX2) so the CPU oracle's fmaf is a single
 # instruction; device code: gfx950.
 COMMON  := $(CXXSTD) -O3 -fPIC -Wall -Wno-unused-result -Icsrc/include -mfma -mavx2 \
-           -fopenmp -D__HIP_PLATFORM_AMD__
+           -fopenmp
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LDFLAGS := -fopenmp -L$(ROCM)/lib -lrccl -ldl -Wl,-rpath,$(ROCM)/lib
 
