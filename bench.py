@@ -27,7 +27,7 @@ non-zero.
 
 Multi-GPU autotune (`--no-autotune` skips it): before the warmup, every
 decomposition candidate (rows slabs, the 2-D MPI_Dims_create grid) x pass
-schedule (deep-halo sync with the default and a doubled exchange interval,
+schedule (deep-halo sync with the default and a halved exchange interval,
 boundary-first pipeline overlapping the exchange with the interior) is timed
 for two steps on the real ranks (max over ranks) and the fastest is
 benchmarked; the table is in the JSON line ("autotune") and the
@@ -91,7 +91,7 @@ def main() -> int:
                          "(use --decomp/--schedule as given)")
     ap.add_argument("--autotune-schedules", default="sync,pipeline",
                     help="comma list of pass schedules the multi-GPU autotune tries")
-    ap.add_argument("--autotune-halo-passes", default="0,16",
+    ap.add_argument("--autotune-halo-passes", default="0,4",
                     help="comma list of sync-schedule passes per exchange (0 = engine default)")
     ap.add_argument("--watchdog-s", type=float, default=900.0,
                     help="abort (stack dump, exit 1) if one phase takes longer than this")

@@ -83,6 +83,9 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 // Variant a launch of `depth` uses by default (HEAT_TB_VARIANT overrides).
 int tb_default_variant(int depth);
+// Variant tb_step picks for a launch of `depth` with this much work
+// (strip-rows of 232/256-column float4 strips per SIMD).
+int tb_auto_variant(int depth, int64_t strip_rows_per_simd);
 // Diagnostics: while set, every tb_step launch writes 4 u64 per wave into buf
 // ({start, end} s_memrealtime ticks (100 MHz), block, strip<<32 | chunk);
 // waves = buffer capacity in waves.  nullptr switches it off.

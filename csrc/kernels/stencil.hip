@@ -272,18 +272,35 @@ int tb_resident_waves(int depth, int variant) {
   return w;
 }
 
-int tb_default_variant(int depth) {
+namespace {
+int tb_env_variant() {
   static const int env = [] {
     const char* e = std::getenv("HEAT_TB_VARIANT");
     return e && *e ? std::atoi(e) : -1;
   }();
-  if (env >= 0) return env;
+  return env;
+}
+}  // namespace
+
+int tb_default_variant(int depth) {
+  if (tb_env_variant() >= 0) return tb_env_variant();
   // Ring-3 + ramp skip, scalar build, XCD-grouped blocks (23); at depth 12
-  // (tall blocks) as two-wave level-split pipelines with ds_bpermute lane
-  // shifts (2071): +5 % in bench.py, +9-10 % in the interleaved kernel A/B
-  // (profiles/tb_wave_timeline_r1.md).  On the short slabs of many-GPU runs
-  // (depth 8) the split form loses, so 23 stays.
+  // on large launches as two-wave level-split pipelines with ds_bpermute
+  // lane shifts (2071): +5 % in bench.py, +9-10 % in the interleaved kernel
+  // A/B (profiles/tb_wave_timeline_r1.md).  tb_step picks per launch from
+  // the work size (tb_auto_variant).
   return depth == kTbDeepDepth ? 2071 : 23;
+}
+
+int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
+  if (tb_env_variant() >= 0) return tb_env_variant();
+  // The split pipelines need about 64 strip-rows per SIMD to pay for their
+  // second wave: below that (the per-rank blocks of 4-8 GPU runs: 1024 x
+  // 8192, 2048 x 4096, 1536 x 8192, ...) one wave per (strip, chunk) at
+  // depth 12 is 8-12 % faster, above it the split is 2-4 % faster
+  // (profiles/tb_block_shapes_r2.md).
+  if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return 23;
+  return tb_default_variant(depth);
 }
 
 void init_field(float* origin, const Layout& L, int64_t gx0, int64_t gy0, int64_t nx, int64_t ny,
@@ -317,7 +334,14 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
-  if (variant < 0) variant = tb_default_variant(depth);
+  if (variant < 0) {
+    // Both defaults use float4 lanes (same strip width).
+    const int W4 = tb_strip_width(depth, 4);
+    int64_t rows4 = 0;
+    for (int b = 0; b < nbox; ++b)
+      if (!boxes[b].empty()) rows4 += ceil_div(boxes[b].cols(), W4) * boxes[b].rows();
+    variant = tb_auto_variant(depth, rows4 / tb_simd_count());
+  }
   const int lag = tb_variant_lag(variant);
   const int W = tb_strip_width(depth, tb_lane_cols(variant));
   int64_t total_strip_rows = 0;

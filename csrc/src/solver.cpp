@@ -217,16 +217,18 @@ int64_t Solver::configured_steps(int64_t steps) const {
 }
 
 int Solver::auto_tb_depth() const {
-  // Depth 12 (2/3 the HBM bytes per update of 8; the level-split pipelines
-  // of tb_default_variant) wins from 2048-row blocks up (+5 % there, +10 %
-  // at 4096+), depth 8 on 1024-row blocks, where the longer ramp of the
-  // shorter chunks costs more than the bytes it saves
-  // (profiles/tb_depth_sweep_r1.md, tb_small_slab_sweep_r1.jsonl).  Decided
-  // from the smallest block of any rank, so every rank picks the same depth.
+  // Depth 12 (2/3 the HBM bytes per update of 8) wins on every per-rank
+  // block of an 8192^2 run on 1-8 GPUs once the variant follows the work
+  // size (tb_auto_variant: level-split pipelines on large launches, one wave
+  // per chunk on small ones): +8 % at 1024 x 8192, +12 % at 2048 x 4096 over
+  // the depth-8 / always-split choice of round 1
+  // (profiles/tb_block_shapes_r2.md).  Thin blocks keep depth 8 (halo
+  // depth, ramp).  Decided from the smallest block of any rank, so every
+  // rank picks the same depth.
   if (!gpu::tb_variant_deep(gpu::tb_default_variant(gpu::kTbDeepDepth))) return 8;
   int64_t min_lx = INT64_MAX;
   for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
-  return min_lx >= 2048 ? gpu::kTbDeepDepth : 8;
+  return min_lx >= 1024 ? gpu::kTbDeepDepth : 8;
 }
 
 std::vector<int> Solver::pass_depths(int64_t n) const {

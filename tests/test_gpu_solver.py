@@ -40,15 +40,15 @@ def test_gpu_depth12_passes(gpu, steps):
 
 
 def test_gpu_auto_depth_tall_block(gpu):
-    # Blocks of >= 2048 rows get depth 12 by default, shorter ones depth 8.
-    tall = HeatConfig(nx=2100, ny=70, steps=30, init="random", seed=6, backend="hip")
+    # Blocks of >= 1024 rows get depth 12 by default, shorter ones depth 8.
+    tall = HeatConfig(nx=1100, ny=70, steps=30, init="random", seed=6, backend="hip")
     with HeatSolver(tall) as s:
         assert s.info.tb_depth == 12
         s.run()
         g = s.gather()
     c, _ = _run(tall.replace(backend="cpu"))
     assert np.array_equal(g, c)
-    with HeatSolver(tall.replace(nx=2000)) as s:
+    with HeatSolver(tall.replace(nx=1000)) as s:
         assert s.info.tb_depth == 8
 
 
