@@ -109,6 +109,16 @@ int tb_auto_waves_per_simd(int depth, int64_t strip_rows_per_simd, int max_per_s
 
 // Copy a box of a strided field to/from a contiguous buffer (E/W halos).
 void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hipStream_t st);
+// Up to kMaxBoxCopies boxes <-> their contiguous buffers (row-major
+// rows x cols) in ONE launch: the packing / unpacking of a whole halo
+// exchange (E/W columns and ghost corners).
+constexpr int kMaxBoxCopies = 8;
+struct BoxCopy {
+  Box box;
+  float* buf = nullptr;
+};
+void copy_boxes(float* origin, int64_t pitch, const BoxCopy* copies, int n, bool to_buf,
+                hipStream_t st);
 void unpack_box(const float* buf, float* origin, int64_t pitch, const Box& box, hipStream_t st);
 
 // Order-independent checksum of the owned block, accumulated on the device

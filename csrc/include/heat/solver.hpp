@@ -150,9 +150,12 @@ class Solver {
   float* field_[2] = {nullptr, nullptr};
   // Contiguous E/W halo buffers (send W, send E, recv W, recv E).
   float* ew_[4] = {nullptr, nullptr, nullptr, nullptr};
-  // Host staging (staged_ mode).
-  float* stage_send_[4] = {nullptr, nullptr, nullptr, nullptr};
-  float* stage_recv_[4] = {nullptr, nullptr, nullptr, nullptr};
+  // Ghost-corner buffers of 2-D grids (send NW NE SW SE, recv NW NE SW SE).
+  float* cn_[8] = {};
+  // Host staging (staged_ mode), one pair per message of an exchange.
+  static constexpr int kMaxMsgs = 8;
+  float* stage_send_[kMaxMsgs] = {};
+  float* stage_recv_[kMaxMsgs] = {};
   size_t stage_bytes_ = 0;
 
   // GPU state.

@@ -29,6 +29,9 @@ std::vector<int> dims_create(int nnodes, int ndims);
 // east/west for dim 1 with east = coord-1 (mpi/...c:68-69); we use the
 // geographic convention west = lower column index.
 enum Dir : int { North = 0, South = 1, West = 2, East = 3 };
+// Diagonal neighbours (2-D grids): the owners of the ghost corners that deep
+// (k > 1) halos need.
+enum Diag : int { NorthWest = 0, NorthEast = 1, SouthWest = 2, SouthEast = 3 };
 
 struct Cart {
   int world = 1;
@@ -41,6 +44,7 @@ struct Cart {
   std::array<int, 2> coords(int rank) const { return {rank / py, rank % py}; }
   int rank_of(int cx, int cy) const;  // kNoNeighbor if outside (non-periodic)
   std::array<int, 4> neighbors(int rank) const;
+  std::array<int, 4> diagonal_neighbors(int rank) const;
 };
 
 // 1-D block partition with remainder distribution: the first (n % p) parts
@@ -57,6 +61,7 @@ struct Block {
   int64_t ox = 0, oy = 0;  // global coordinates of the first owned cell
   int64_t lx = 0, ly = 0;  // owned extent
   std::array<int, 4> nbr{kNoNeighbor, kNoNeighbor, kNoNeighbor, kNoNeighbor};
+  std::array<int, 4> diag{kNoNeighbor, kNoNeighbor, kNoNeighbor, kNoNeighbor};
 };
 
 Block make_block(const Cart& cart, int rank, int64_t nx, int64_t ny);

@@ -88,6 +88,27 @@ __global__ void pack_kernel(const float* __restrict__ origin, int64_t pitch, Box
   }
 }
 
+struct BoxCopies {
+  BoxCopy c[kMaxBoxCopies];
+};
+
+// blockIdx.y selects the box; rows are grid-strided over blockIdx.x, columns
+// over the threads (row segments are contiguous in both the field and the
+// buffer).
+__global__ __launch_bounds__(128) void box_copy_kernel(float* __restrict__ origin, int64_t pitch,
+                                                       BoxCopies a, int to_buf) {
+  const BoxCopy& c = a.c[blockIdx.y];
+  const int64_t rows = c.box.r1 - c.box.r0, cols = c.box.c1 - c.box.c0;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    float* f = origin + (c.box.r0 + r) * pitch + c.box.c0;
+    float* b = c.buf + r * cols;
+    for (int64_t j = threadIdx.x; j < cols; j += blockDim.x) {
+      if (to_buf) b[j] = f[j];
+      else f[j] = b[j];
+    }
+  }
+}
+
 __global__ void unpack_kernel(const float* __restrict__ buf, float* __restrict__ origin,
                               int64_t pitch, Box box) {
   const int64_t cols = box.c1 - box.c0, n = (box.r1 - box.r0) * cols;
@@ -479,6 +500,23 @@ void pack_box(const float* origin, int64_t pitch, const Box& box, float* buf, hi
   if (box.empty()) return;
   hipLaunchKernelGGL(pack_kernel, dim3(grid_1d(box.rows() * box.cols())), dim3(256), 0, st,
                      origin, pitch, box, buf);
+  HIP_CHECK(hipGetLastError());
+}
+
+void copy_boxes(float* origin, int64_t pitch, const BoxCopy* copies, int n, bool to_buf,
+                hipStream_t st) {
+  HEAT_CHECK(n >= 0 && n <= kMaxBoxCopies, "copy_boxes: %d boxes", n);
+  BoxCopies a{};
+  int m = 0;
+  int64_t rows = 0;
+  for (int i = 0; i < n; ++i) {
+    if (copies[i].box.empty()) continue;
+    a.c[m++] = copies[i];
+    rows = std::max(rows, copies[i].box.rows());
+  }
+  if (m == 0) return;
+  dim3 grid(unsigned(std::min<int64_t>(rows, 2048)), unsigned(m));
+  hipLaunchKernelGGL(box_copy_kernel, grid, dim3(128), 0, st, origin, pitch, a, int(to_buf));
   HIP_CHECK(hipGetLastError());
 }
 

@@ -121,6 +121,8 @@ void Solver::alloc() {
     }
     if (cart_.py > 1)
       for (auto& b : ew_) HIP_CHECK(hipMalloc(&b, ew_elems * 4));
+    if (cart_.px > 1 && cart_.py > 1)
+      for (auto& b : cn_) HIP_CHECK(hipMalloc(&b, size_t(H_) * size_t(H_) * 4));
     HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     {
       // The comm stream gets the highest priority so RCCL's kernels are
@@ -137,7 +139,7 @@ void Solver::alloc() {
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
     if (staged_) {
       stage_bytes_ = std::max<size_t>(size_t(H_) * size_t(L_.pitch), ew_elems) * 4;
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kMaxMsgs; ++i) {
         HIP_CHECK(hipHostMalloc(&stage_send_[i], stage_bytes_));
         HIP_CHECK(hipHostMalloc(&stage_recv_[i], stage_bytes_));
       }
@@ -154,6 +156,11 @@ void Solver::alloc() {
         b = static_cast<float*>(std::malloc(ew_elems * 4));
         HEAT_CHECK(b != nullptr, "host allocation failed");
       }
+    if (cart_.px > 1 && cart_.py > 1)
+      for (auto& b : cn_) {
+        b = static_cast<float*>(std::malloc(size_t(H_) * size_t(H_) * 4));
+        HEAT_CHECK(b != nullptr, "host allocation failed");
+      }
   }
 }
 
@@ -168,7 +175,9 @@ void Solver::free_all() {
       if (b) (void)hipFree(b);
     for (auto& b : ew_)
       if (b) (void)hipFree(b);
-    for (int i = 0; i < 4; ++i) {
+    for (auto& b : cn_)
+      if (b) (void)hipFree(b);
+    for (int i = 0; i < kMaxMsgs; ++i) {
       if (stage_send_[i]) (void)hipHostFree(stage_send_[i]);
       if (stage_recv_[i]) (void)hipHostFree(stage_recv_[i]);
     }
@@ -185,10 +194,12 @@ void Solver::free_all() {
   } else {
     for (auto& b : base_) std::free(b);
     for (auto& b : ew_) std::free(b);
+    for (auto& b : cn_) std::free(b);
   }
   for (auto& b : base_) b = nullptr;
   for (auto& b : ew_) b = nullptr;
-  for (int i = 0; i < 4; ++i) stage_send_[i] = stage_recv_[i] = nullptr;
+  for (auto& b : cn_) b = nullptr;
+  for (int i = 0; i < kMaxMsgs; ++i) stage_send_[i] = stage_recv_[i] = nullptr;
   d_resid_ = nullptr;
   h_resid_ = nullptr;
   d_scratch_ = d_checksum_ = nullptr;
@@ -281,6 +292,7 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
     }
     // GPU fields, host transport: stage through pinned host memory.
     std::vector<Msg> host(msgs.size());
+    HEAT_CHECK(int(msgs.size()) <= kMaxMsgs, "%zu messages", msgs.size());
     for (size_t i = 0; i < msgs.size(); ++i) {
       HEAT_CHECK(msgs[i].sbytes <= stage_bytes_ && msgs[i].rbytes <= stage_bytes_, "stage size");
       host[i] = Msg{msgs[i].peer, stage_send_[i], msgs[i].sbytes, stage_recv_[i], msgs[i].rbytes};
@@ -308,43 +320,55 @@ void Solver::exchange(int buf, int k, hipStream_t st) {
                                  hipMemcpyHostToDevice, st));
   };
 
-  // Phase 1: west/east columns of the owned rows (packed).
-  if (nb[West] >= 0 || nb[East] >= 0) {
-    const size_t bytes = size_t(lx) * size_t(k) * 4;
-    const Box sw{0, lx, 0, k}, se{0, lx, ly - k, ly}, rw{0, lx, -k, 0}, re{0, lx, ly, ly + k};
-    std::vector<Msg> msgs;
-    if (nb[West] >= 0) {
-      if (gpu) gpu::pack_box(f, pitch, sw, ew_[0], st);
-      else host_pack(f, pitch, sw, ew_[0]);
-      msgs.push_back(Msg{nb[West], ew_[0], bytes, ew_[2], bytes});
-    }
-    if (nb[East] >= 0) {
-      if (gpu) gpu::pack_box(f, pitch, se, ew_[1], st);
-      else host_pack(f, pitch, se, ew_[1]);
-      msgs.push_back(Msg{nb[East], ew_[1], bytes, ew_[3], bytes});
-    }
-    do_sendrecv(msgs);
-    if (nb[West] >= 0) {
-      if (gpu) gpu::unpack_box(ew_[2], f, pitch, rw, st);
-      else host_unpack(ew_[2], f, pitch, rw);
-    }
-    if (nb[East] >= 0) {
-      if (gpu) gpu::unpack_box(ew_[3], f, pitch, re, st);
-      else host_unpack(ew_[3], f, pitch, re);
-    }
+  // One phase, every message of the exchange in one group (one RCCL
+  // latency): packed W/E columns of the owned rows, the N/S neighbours' rows
+  // as full padded rows straight into the ghost rows, and on 2-D grids the
+  // four k x k ghost corners from the diagonal neighbours, which deep (k > 1)
+  // halos need.  A received N/S row also carries the sender's (stale) ghost
+  // columns into our corner columns; the corner unpack after the group
+  // overwrites them.  (The reference exchanges 1-deep halos, no corners,
+  // mpi/mpi_heat_improved_persistent_stat.c:130-161.)
+  const Box sw{0, lx, 0, k}, se{0, lx, ly - k, ly}, rw{0, lx, -k, 0}, re{0, lx, ly, ly + k};
+  const Box csend[4] = {{0, k, 0, k}, {0, k, ly - k, ly}, {lx - k, lx, 0, k}, {lx - k, lx, ly - k, ly}};
+  const Box crecv[4] = {{-k, 0, -k, 0}, {-k, 0, ly, ly + k}, {lx, lx + k, -k, 0}, {lx, lx + k, ly, ly + k}};
+  std::vector<Msg> msgs;
+  gpu::BoxCopy pk[6], uk[6];
+  int np = 0, nu = 0;
+  const size_t ew_bytes = size_t(lx) * size_t(k) * 4, c_bytes = size_t(k) * size_t(k) * 4;
+  if (nb[West] >= 0) {
+    pk[np++] = {sw, ew_[0]};
+    uk[nu++] = {rw, ew_[2]};
+    msgs.push_back(Msg{nb[West], ew_[0], ew_bytes, ew_[2], ew_bytes});
   }
-  // Phase 2: north/south full padded rows (contiguous, no packing).  They
-  // include the just-received W/E ghost columns, which fills the corners
-  // that k > 1 deep halos need.
+  if (nb[East] >= 0) {
+    pk[np++] = {se, ew_[1]};
+    uk[nu++] = {re, ew_[3]};
+    msgs.push_back(Msg{nb[East], ew_[1], ew_bytes, ew_[3], ew_bytes});
+  }
+  for (int d = 0; d < 4; ++d) {
+    if (blk_.diag[d] < 0) continue;
+    pk[np++] = {csend[d], cn_[d]};
+    uk[nu++] = {crecv[d], cn_[4 + d]};
+    msgs.push_back(Msg{blk_.diag[d], cn_[d], c_bytes, cn_[4 + d], c_bytes});
+  }
   if (nb[North] >= 0 || nb[South] >= 0) {
     const size_t bytes = size_t(k) * size_t(pitch) * 4;
     const int64_t hy = L_.hy;
-    std::vector<Msg> msgs;
     if (nb[North] >= 0)
       msgs.push_back(Msg{nb[North], f - hy, bytes, f - k * pitch - hy, bytes});
     if (nb[South] >= 0)
       msgs.push_back(Msg{nb[South], f + (lx - k) * pitch - hy, bytes, f + lx * pitch - hy, bytes});
-    do_sendrecv(msgs);
+  }
+  if (gpu) {
+    gpu::copy_boxes(f, pitch, pk, np, true, st);
+  } else {
+    for (int i = 0; i < np; ++i) host_pack(f, pitch, pk[i].box, pk[i].buf);
+  }
+  do_sendrecv(msgs);
+  if (gpu) {
+    gpu::copy_boxes(f, pitch, uk, nu, false, st);
+  } else {
+    for (int i = 0; i < nu; ++i) host_unpack(uk[i].buf, f, pitch, uk[i].box);
   }
   ++stat_exchanges_;
 }

@@ -72,6 +72,16 @@ std::array<int, 4> Cart::neighbors(int rank) const {
   return n;
 }
 
+std::array<int, 4> Cart::diagonal_neighbors(int rank) const {
+  auto c = coords(rank);
+  std::array<int, 4> n{};
+  n[NorthWest] = rank_of(c[0] - 1, c[1] - 1);
+  n[NorthEast] = rank_of(c[0] - 1, c[1] + 1);
+  n[SouthWest] = rank_of(c[0] + 1, c[1] - 1);
+  n[SouthEast] = rank_of(c[0] + 1, c[1] + 1);
+  return n;
+}
+
 Span block_span(int64_t n, int parts, int index) {
   HEAT_CHECK(parts >= 1 && index >= 0 && index < parts, "parts=%d index=%d", parts, index);
   const int64_t base = n / parts, rem = n % parts;
@@ -95,6 +105,7 @@ Block make_block(const Cart& cart, int rank, int64_t nx, int64_t ny) {
   b.oy = sy.offset;
   b.ly = sy.size;
   b.nbr = cart.neighbors(rank);
+  b.diag = cart.diagonal_neighbors(rank);
   return b;
 }
 

@@ -96,6 +96,13 @@ class Cart:
         return (self.rank_of(cx - 1, cy), self.rank_of(cx + 1, cy),
                 self.rank_of(cx, cy - 1), self.rank_of(cx, cy + 1))
 
+    def diagonal_neighbors(self, rank: int) -> Tuple[int, int, int, int]:
+        """(NW, NE, SW, SE): the owners of the ghost corners of deep halos
+        (heat::Cart::diagonal_neighbors)."""
+        cx, cy = self.coords(rank)
+        return (self.rank_of(cx - 1, cy - 1), self.rank_of(cx - 1, cy + 1),
+                self.rank_of(cx + 1, cy - 1), self.rank_of(cx + 1, cy + 1))
+
     def block(self, rank: int, nx: int, ny: int) -> Block:
         cx, cy = self.coords(rank)
         ox, lx = block_span(nx, self.px, cx)

@@ -29,6 +29,7 @@ def single(base, steps):
     (2, dict(decomp="rows", schedule="sync")),
     (2, dict(px=1, py=2, schedule="overlap")),
     (3, dict(decomp="rows", schedule="pipeline")),
+    (4, dict(px=2, py=2, schedule="sync")),  # ghost corners from the diagonal ranks
     (2, dict(decomp="rows", schedule="sync", use_graph=False)),
 ])
 def test_rccl_ranks_one_device(gpu, tmp_path, world, kw):

@@ -65,6 +65,21 @@ def test_cart_neighbours_row_major():
     assert c.neighbors(0) == (T.NO_NEIGHBOR, 2, T.NO_NEIGHBOR, 1)
 
 
+def test_cart_diagonal_neighbours():
+    c = T.Cart.create(8)  # dims [4, 2]
+    assert c.diagonal_neighbors(5) == (2, T.NO_NEIGHBOR, 6, T.NO_NEIGHBOR)
+    assert c.diagonal_neighbors(0) == (T.NO_NEIGHBOR,) * 3 + (3,)
+    # Every diagonal pair is mutual and distinct from the edge neighbours
+    # (one message per peer per exchange).
+    for r in range(8):
+        d = c.diagonal_neighbors(r)
+        for k, q in enumerate(d):
+            if q != T.NO_NEIGHBOR:
+                assert c.diagonal_neighbors(q)[3 - k] == r
+                assert q not in c.neighbors(r)
+    assert T.Cart.create(8, "rows").diagonal_neighbors(3) == (T.NO_NEIGHBOR,) * 4
+
+
 def test_cart_rows_and_explicit():
     assert (T.Cart.create(8, "rows").px, T.Cart.create(8, "rows").py) == (8, 1)
     c = T.Cart.create(6, px=1, py=6)

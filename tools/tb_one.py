@@ -15,11 +15,15 @@ ap.add_argument("--depth", type=int, default=8)
 ap.add_argument("--variant", type=int, default=2)
 ap.add_argument("--waves", type=int, default=0)
 ap.add_argument("--launches", type=int, default=10)
+ap.add_argument("--nx", type=int, default=0, help="rows (default --n)")
+ap.add_argument("--interior", action="store_true",
+                help="the block sits inside a larger plate (a middle rank's block)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
-g = ops.Geom(nx=a.n, ny=a.n)
-x = ops.Field(a.n, a.n, a.depth, dev)
-y = ops.Field(a.n, a.n, a.depth, dev)
+nx = a.nx or a.n
+g = ops.Geom(nx=nx, ny=a.n) if not a.interior else ops.Geom(nx=4 * nx, ny=4 * a.n, gx0=nx, gy0=a.n)
+x = ops.Field(nx, a.n, a.depth, dev)
+y = ops.Field(nx, a.n, a.depth, dev)
 ops.init_field(x, g, "random", 1)
 ops.init_field(y, g, "random", 1)
 for i in range(a.launches):
