@@ -368,12 +368,17 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   int64_t total_strip_rows = 0;
   for (int b = 0; b < nbox; ++b)
     if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
-  // Age pairs (kTbAgePairs) for launches of exactly two waves per SIMD
-  // chosen by the planner; HEAT_TB_AGE_RATIO = older:younger rows (<= 1: off).
-  static const double age_ratio = [] {
+  // Age pairs (kTbAgePairs) for launches of exactly two waves (or two-wave
+  // pipelines) per SIMD chosen by the planner; HEAT_TB_AGE_RATIO =
+  // older:younger rows (<= 1: off) overrides the defaults (kTbAgeRatio for
+  // single-wave pipelines, kTbSplitAgeRatio for the level-split ones).
+  static const double env_age_ratio = [] {
     const char* e = std::getenv("HEAT_TB_AGE_RATIO");
-    return e && *e ? std::atof(e) : kTbAgeRatio;
+    return e && *e ? std::atof(e) : -1.0;
   }();
+  const double age_ratio = env_age_ratio >= 0.0 ? env_age_ratio
+                           : tb_variant_split(variant) ? kTbSplitAgeRatio
+                                                       : kTbAgeRatio;
   bool pairs = (variant & 256) != 0;  // bit 256: force age pairs (tests)
   if (waves_target <= 0) {
     // Whole rounds of the resident wave capacity (a partial last round leaves
@@ -388,7 +393,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       const int per_simd = tb_auto_waves_per_simd(depth, total_strip_rows / simds,
                                                   std::max(1, resident / simds));
       waves_target = simds * per_simd;
-      pairs = pairs || (per_simd == 2 && age_ratio > 1.0 && !(variant & 64));
+      // Bit 16384: never pair (A/B of the age ratio in one process).
+      pairs = pairs || (per_simd == 2 && age_ratio > 1.0 && !(variant & 64) && !(variant & 16384));
     }
   }
   TbArgs args{};
