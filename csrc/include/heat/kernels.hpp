@@ -39,10 +39,10 @@ constexpr int kTbMaxDepth = 8;    // 1..8: every build
 // launch span, which the SIMD's combined issue rate sets
 // (profiles/tb_wave_timeline_r1.md).
 constexpr double kTbAgeRatio = 1.0;
-// Level-split pipelines at two per SIMD: the older pipeline of each chunk
-// pair takes 1.7x the rows of the younger one: +4-7 % at 2048..8192-row
-// blocks in the same-process A/B (profiles/tb_split_age_pairs_r2.md).
-constexpr double kTbSplitAgeRatio = 1.7;
+// Level-split pipelines at two per SIMD: the first-dispatched half of the
+// grid takes 1.7x the rows of the second half in each pair of adjacent
+// chunks: +4-7 % at 2048..8192-row blocks (profiles/tb_split_age_pairs_r2.md).
+constexpr double kTbSplitAgeWeights[2] = {1.7, 1.0};
 constexpr int kTbDeepDepth = 12;  // + 12: scalar ring-3+ramp build (variant bits 4|3)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.

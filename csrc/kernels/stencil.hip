@@ -19,11 +19,14 @@
 //    results are bitwise equal across kernels, depths and decompositions.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <vector>
 
 #include "heat/common.hpp"
 #include "heat/init_fn.hpp"
@@ -368,18 +371,51 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   int64_t total_strip_rows = 0;
   for (int b = 0; b < nbox; ++b)
     if (!boxes[b].empty()) total_strip_rows += ceil_div(boxes[b].cols(), W) * boxes[b].rows();
-  // Age pairs (kTbAgePairs) for launches of exactly two waves (or two-wave
-  // pipelines) per SIMD chosen by the planner; HEAT_TB_AGE_RATIO =
-  // older:younger rows (<= 1: off) overrides the defaults (kTbAgeRatio for
-  // single-wave pipelines, kTbSplitAgeRatio for the level-split ones).
-  static const double env_age_ratio = [] {
-    const char* e = std::getenv("HEAT_TB_AGE_RATIO");
-    return e && *e ? std::atof(e) : -1.0;
+  // Age groups (kTbAgePairs) for launches of whole resident rounds: blocks
+  // dispatched earlier issue faster (the SIMD's arbitration favours older
+  // waves), so the grid is split into G parts (part a = the a-th share of
+  // the dispatch rounds) and older parts get more rows.  Default: two parts
+  // at kTbSplitAgeWeights for the level-split pipelines; none (kTbAgeRatio
+  // = 1) for single-wave pipelines.  HEAT_TB_AGE_WEIGHTS="w0,w1,..." (2-4
+  // parts) or HEAT_TB_AGE_RATIO=r (two parts r : 1) override; "1" = off.
+  // Four parts (one per round at 4 blocks per CU) measured slower than two
+  // whatever the weights (profiles/tb_split_age_pairs_r2.md).
+  static const std::vector<double> env_weights = [] {
+    std::vector<double> w;
+    if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
+      for (const char* q = e; *q;) {
+        char* end = nullptr;
+        const double v = std::strtod(q, &end);
+        if (end == q) break;
+        w.push_back(v);
+        q = *end == ',' ? end + 1 : end;
+      }
+    } else if (const char* r = std::getenv("HEAT_TB_AGE_RATIO"); r && *r) {
+      w = {std::atof(r), 1.0};
+    }
+    return w;
   }();
-  const double age_ratio = env_age_ratio >= 0.0 ? env_age_ratio
-                           : tb_variant_split(variant) ? kTbSplitAgeRatio
-                                                       : kTbAgeRatio;
-  bool pairs = (variant & 256) != 0;  // bit 256: force age pairs (tests)
+  const bool split_v = tb_variant_split(variant);
+  int G = 0;  // age groups of this launch (0: none)
+  std::vector<double> weights;
+  auto set_weights = [&](int max_groups) {
+    if (!env_weights.empty())
+      weights = env_weights;
+    else if (split_v)
+      weights.assign(std::begin(kTbSplitAgeWeights), std::end(kTbSplitAgeWeights));
+    else
+      weights = {kTbAgeRatio, 1.0};
+    bool uneven = false;
+    for (double w : weights) uneven = uneven || w != weights[0] || w <= 0.0;
+    G = uneven && int(weights.size()) >= 2 && int(weights.size()) <= max_groups ? int(weights.size()) : 0;
+  };
+  if (variant & 256) {  // bit 256: force age groups (tests); even weights still group
+    set_weights(4);
+    if (G == 0) {
+      G = 2;
+      weights.assign(2, 1.0);
+    }
+  }
   if (waves_target <= 0) {
     // Whole rounds of the resident wave capacity (a partial last round leaves
     // SIMDs idle for the tail of the launch); by default with the number of
@@ -393,10 +429,15 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       const int per_simd = tb_auto_waves_per_simd(depth, total_strip_rows / simds,
                                                   std::max(1, resident / simds));
       waves_target = simds * per_simd;
-      // Bit 16384: never pair (A/B of the age ratio in one process).
-      pairs = pairs || (per_simd == 2 && age_ratio > 1.0 && !(variant & 64) && !(variant & 16384));
+      // Blocks per CU = dispatch rounds: single-wave pipelines put one wave
+      // per SIMD in a block, level-split blocks hold two pipelines (4 waves).
+      const int blocks_per_cu = split_v ? 2 * per_simd : per_simd;
+      // Bit 16384: never group (A/B of the weights in one process).
+      if (G == 0 && blocks_per_cu >= 2 && !(variant & 64) && !(variant & 16384))
+        set_weights(blocks_per_cu);
     }
   }
+  const bool pairs = G > 0;
   TbArgs args{};
   args.src = src;
   args.dst = dst;
@@ -437,15 +478,14 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       t.nstrips = int(ceil_div(B.cols(), W));
       t.chunk_len = int(std::min<int64_t>(clen, B.rows()));
       t.nchunks = int(ceil_div(B.rows(), t.chunk_len));
-      t.age_delta = 0;
       if (pairs) {
-        // Units are chunk pairs (2 * chunk_len rows), one wave of each half.
-        t.chunk_len = int(std::max<int64_t>(1, ceil_div(std::min<int64_t>(2 * clen, B.rows()), 2)));
-        t.nchunks = int(ceil_div(B.rows(), 2 * int64_t(t.chunk_len)));
-        t.age_delta = int(double(t.chunk_len) * (age_ratio - 1.0) / (age_ratio + 1.0));
+        // Units are groups of G chunks (G * chunk_len rows), one wave (or
+        // pipeline) of each age.
+        t.chunk_len = int(std::max<int64_t>(1, ceil_div(std::min<int64_t>(G * clen, B.rows()), G)));
+        t.nchunks = int(ceil_div(B.rows(), G * int64_t(t.chunk_len)));
       }
       t.wave_begin = waves;
-      waves += t.nstrips * t.nchunks * (pairs ? 2 : 1);
+      waves += t.nstrips * t.nchunks * (pairs ? G : 1);
     };
     for (int b = 0; b < nbox; ++b) {
       const Box& B = boxes[b];
@@ -481,10 +521,19 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.nbox = n;
   args.total_waves = waves;
   if (pairs) {
-    // wave_begin / total_waves count pairs (waves of one half).
-    for (int b = 0; b < n; ++b) args.box[b].wave_begin /= 2;
-    args.total_waves = waves / 2;
+    // wave_begin / total_waves count groups (units of one age).
+    for (int b = 0; b < n; ++b) args.box[b].wave_begin /= G;
+    args.total_waves = waves / G;
     args.flags |= tbdetail::kTbAgePairs;
+    args.age_groups = G;
+    double tot = 0.0;
+    for (double w : weights) tot += w;
+    double acc = 0.0;
+    args.age_cum[0] = 0;
+    for (int a = 0; a < G; ++a) {
+      acc += weights[size_t(a)];
+      args.age_cum[a + 1] = a + 1 == G ? 1024 : int(std::lround(1024.0 * acc / tot));
+    }
   }
   const bool split = tb_variant_split(variant);
   if (g_tb_stamps) {

@@ -13,7 +13,6 @@ namespace heat::gpu::tbdetail {
 struct TbBox {
   int64_t r0, r1, c0, c1;
   int nstrips, nchunks, chunk_len, wave_begin;
-  int age_delta;  // kTbAgePairs: extra rows of the older wave of a chunk pair
 };
 
 constexpr int kMaxBoxes = 16;
@@ -26,7 +25,12 @@ struct TbArgs {
   unsigned* resid;
   StencilGeom g;
   int nbox, total_waves;
-  int flags;  // kTbXcdGroups | kTbAltDirection
+  int flags;  // kTbXcdGroups | kTbAltDirection | kTbAgePairs ...
+  // kTbAgePairs: the grid is age_groups equal parts (dispatch rounds); a
+  // group of age_groups vertically adjacent chunks is split between one unit
+  // of each part at the cumulative row fractions age_cum[a] / 1024.
+  int age_groups;
+  int age_cum[5];
   // Diagnostics (null in production): per wave {start, end} of the global
   // 100 MHz s_memrealtime clock, block<<40 | XCC_ID<<32 | HW_ID and
   // strip<<32 | chunk, 4 u64
@@ -44,11 +48,13 @@ struct TbArgs {
 //                    time (both at the start or both at the end).
 constexpr int kTbXcdGroups = 1;
 constexpr int kTbAltDirection = 2;
-//   kTbAgePairs      two waves per SIMD split each pair of adjacent chunks
-//                    unevenly, the older (first-dispatched) wave taking more
-//                    rows: with equal chunks the older wave finishes at ~60 %
-//                    of the launch and the younger one runs the rest alone
-//                    (tools/wave_timeline.py, profiles/tb_age_pairs_r1.md).
+//   kTbAgePairs      age groups: the G blocks a CU holds (dispatch rounds:
+//                    grid part a = round a) split each group of G adjacent
+//                    chunks unevenly, older (earlier-dispatched) blocks taking
+//                    more rows: the SIMD's issue arbitration favours older
+//                    waves, so with equal chunks the youngest set the launch
+//                    tail (tools/wave_timeline.py by_age_rank,
+//                    profiles/tb_split_age_pairs_r2.md).
 constexpr int kTbAgePairs = 4;
 //   kTbDiagNoStore   diagnostics: skip the output stores (wrong results; a
 //                    timing probe of the store traffic; variant bit 1024).

@@ -410,8 +410,8 @@ __device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, 
   int nb = gridDim.x, blk = blockIdx.x;
   age = 0;
   if (pairs) {
-    nb >>= 1;
-    age = blk >= nb;
+    nb /= a.age_groups;  // the launch makes the grid a multiple of age_groups
+    age = min(blk / nb, a.age_groups - 1);
     blk -= age * nb;
   }
   if (a.flags & tbdetail::kTbXcdGroups) {
@@ -448,13 +448,13 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
   int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
   int64_t re = min(rb + bx.chunk_len, bx.r1);
   if (pairs) {
-    // Box chunks are pairs of 2 * chunk_len rows; the older wave takes
-    // chunk_len + delta of them.
-    const int64_t p0 = bx.r0 + int64_t(chunk) * 2 * bx.chunk_len;
-    const int64_t p1 = min(p0 + 2 * int64_t(bx.chunk_len), bx.r1);
-    const int64_t split = min(p0 + bx.chunk_len + bx.age_delta, p1);
-    rb = age ? split : p0;
-    re = age ? p1 : split;
+    // Box chunks are groups of G * chunk_len rows; age a takes rows
+    // [age_cum[a], age_cum[a+1]) / 1024 of its group.
+    const int G = a.age_groups;
+    const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
+    const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
+    rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
+    re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
     if (rb >= re) return;
   }
 
@@ -600,7 +600,9 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_sp
 template <int K, int LAG>
 void launch_k(const TbArgs& args, hipStream_t st) {
   int blocks = int((args.total_waves + 3) / 4);
-  if (args.flags & tbdetail::kTbAgePairs) blocks *= 2;  // two halves, see tb_kernel
+  // Age groups: each grid part a whole number of 8-block XCD rounds, so a
+  // part's local block index has the physical block's XCD (tb_unit).
+  if (args.flags & tbdetail::kTbAgePairs) blocks = (blocks + 7) / 8 * 8 * args.age_groups;
   hipLaunchKernelGGL((tb_kernel<K, LAG>), dim3(blocks), dim3(256), 0, st, args);
 }
 
@@ -700,7 +702,7 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
 template <int K, int K1>
 void launch_split_k(const TbArgs& args, hipStream_t st) {
   int blocks = int((args.total_waves + 1) / 2);  // two pipelines per block
-  if (args.flags & tbdetail::kTbAgePairs) blocks *= 2;
+  if (args.flags & tbdetail::kTbAgePairs) blocks = (blocks + 7) / 8 * 8 * args.age_groups;
   hipLaunchKernelGGL((tb_split_kernel<K, K1>), dim3(blocks), dim3(256), 0, st, args);
 }
 template <int K, int K1>

@@ -85,6 +85,31 @@ def main():
         "first_half_blocks_mean_dur_us": round(float(dur[blk < nb // 2].mean()), 1),
         "second_half_blocks_mean_dur_us": round(float(dur[blk >= nb // 2].mean()), 1),
     }
+    # Age rank of each wave on its SIMD (0 = first-dispatched block) and the
+    # per-SIMD finish times: how the launch tail splits across ages.
+    rank = torch.zeros_like(blk)
+    prev, r = -1, 0
+    for i in range(len(ss)):
+        r = r + 1 if int(ss[i]) == prev else 0
+        prev = int(ss[i])
+        rank[order[i]] = r
+    ages = []
+    for a_ in range(int(rank.max()) + 1):
+        m = rank == a_
+        ages.append({"age": a_, "waves": int(m.sum()), "mean_start_us": round(float(start[m].mean()), 1),
+                     "mean_dur_us": round(float(dur[m].mean()), 1),
+                     "mean_end_us": round(float(end[m].mean()), 1)})
+    out["by_age_rank"] = ages
+    parts = []
+    for q in range(4):  # grid quarters (the age groups of a 4-group launch)
+        m = (blk >= q * nb // 4) & (blk < (q + 1) * nb // 4)
+        parts.append({"quarter": q, "waves": int(m.sum()), "mean_dur_us": round(float(dur[m].mean()), 1),
+                      "mean_rank": round(float(rank[m].double().mean()), 2)})
+    out["by_grid_quarter"] = parts
+    last = torch.zeros(int(slot.max()) + 1, dtype=torch.float64)
+    last.index_reduce_(0, slot, end, "amax", include_self=False)
+    used = last[torch.unique(slot)]
+    out["simd_last_end_p10_p50_p90_us"] = [round(float(used.quantile(q)), 1) for q in (0.1, 0.5, 0.9)]
     print(json.dumps(out))
 
 
