@@ -106,6 +106,13 @@ def main():
         parts.append({"quarter": q, "waves": int(m.sum()), "mean_dur_us": round(float(dur[m].mean()), 1),
                       "mean_rank": round(float(rank[m].double().mean()), 2)})
     out["by_grid_quarter"] = parts
+    # The last waves to finish: what they are.
+    idx = torch.argsort(end, descending=True)[:12]
+    out["last_waves"] = [{"end_us": round(float(end[i]), 1), "dur_us": round(float(dur[i]), 1),
+                          "strip": int(strip[i]), "chunk": int(chunk[i]), "rank": int(rank[i]),
+                          "block": int(blk[i]), "xcc": int(xcc[i])} for i in idx.tolist()]
+    hist = torch.histc(end.float(), bins=10, min=0, max=span)
+    out["end_histogram_10"] = [int(x) for x in hist.tolist()]
     last = torch.zeros(int(slot.max()) + 1, dtype=torch.float64)
     last.index_reduce_(0, slot, end, "amax", include_self=False)
     used = last[torch.unique(slot)]
