@@ -208,6 +208,7 @@ void Solver::free_all() {
 }
 
 void Solver::init_fields() {
+  TraceRange trace("heat.init");
   const int mode = int(P_.init);
   for (int i = 0; i < 2; ++i) {
     if (on_gpu())
@@ -398,6 +399,10 @@ void Solver::check_staged() {
 void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int64_t er,
                          int64_t ec, hipStream_t st) {
   if (!st) st = s_comp_;
+  // Host-side enqueue range (interior / boundary bands of the overlap
+  // schedules, or the whole pass); the kernels' device time is in the
+  // kernel trace.
+  TraceRange trace(!split ? "heat.compute" : part == 0 ? "heat.interior" : "heat.boundary");
   PhaseScope phase(this, kCompute, st);
   const float* src = field_[cur_];
   float* dst = field_[cur_ ^ 1];
@@ -460,6 +465,7 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
 }
 
 void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
+  TraceRange trace("heat.compute");
   PhaseScope phase(this, kCompute, nullptr);
   cpu::Geom g;
   g.pitch = L_.pitch;
@@ -590,6 +596,7 @@ void Solver::enqueue_pass(int k, bool resid) {
     }
     if (tb) cur_ ^= 1;
     if (resid) {
+      TraceRange trace("heat.allreduce");
       PhaseScope phase(this, kReduce, s_comp_);
       if (tr_->device_memory()) tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
       HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
@@ -1009,6 +1016,7 @@ Checksum Solver::checksum() {
 }
 
 void Solver::write_bin(const std::string& path) {
+  TraceRange trace("heat.output");
   // Written as `path`.tmp by every rank, then renamed by rank 0 once all
   // blocks are in: a crash mid-write (a --checkpoint-every run) leaves the
   // previous checkpoint intact.
@@ -1036,6 +1044,7 @@ void Solver::write_bin(const std::string& path) {
 }
 
 void Solver::read_bin(const std::string& path) {
+  TraceRange trace("heat.resume");
   BinHeader h = bin_read_header(path);
   HEAT_CHECK(h.nx == P_.nx && h.ny == P_.ny, "checkpoint is %lldx%lld, run is %lldx%lld",
              (long long)h.nx, (long long)h.ny, (long long)P_.nx, (long long)P_.ny);

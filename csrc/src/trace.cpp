@@ -18,7 +18,12 @@ struct Roctx {
   Roctx() {
     const char* e = std::getenv("HEAT_ROCTX");
     if (e && e[0] == '0') return;
-    void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_LOCAL);
+    // rocprofv3 (rocprofiler-sdk) intercepts the SDK's roctx library; the
+    // legacy roctracer libroctx64 is only a fallback (its ranges are not
+    // seen by rocprofv3 --marker-trace).
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libroctx64.so", RTLD_NOW | RTLD_LOCAL);
     if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
     if (!h) return;
     push = reinterpret_cast<PushFn>(dlsym(h, "roctxRangePushA"));
