@@ -58,6 +58,8 @@ void usage() {
       "  --gpus N                one process, N GPU ranks as threads (loopback/peer copies;\n"
       "                          with --transport rccl: one RCCL rank per GPU)\n"
       "  --phase-timing          per-phase times (exchange/compute/reduce) in --json; eager\n"
+      "  --plan                  print the per-GPU memory plan (fields + halo buffers, worst\n"
+      "                          rank, 288 GB HBM3E check) for --gpus/WORLD_SIZE ranks; exit\n"
       "  --json                  print a JSON metrics line\n");
 }
 
@@ -214,6 +216,7 @@ int main(int argc, char** argv) {
   std::string transport = "auto";
   int gpus = 0;
   bool backend_set = false;
+  bool plan = false;
   int port = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -292,11 +295,40 @@ int main(int argc, char** argv) {
     else if (a == "--json") o.json = true;
     else if (a == "--gpus") gpus = std::atoi(need().c_str());
     else if (a == "--phase-timing") P.phase_timing = true;
+    else if (a == "--plan") plan = true;
     else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
   }
   if (o.naming == "mpi" && P.compat == Compat::None) P.compat = Compat::Mpi;
   if (o.naming == "cuda" && P.compat == Compat::None) P.compat = Compat::Cuda;
 
+  if (plan) {
+    // Memory plan without allocating: the two fields of
+    // every rank's block plus its ghost ring at the deepest halo the solver
+    // picks (depth 12 x 8 passes per exchange = 96, or --tb-depth x
+    // --halo-passes), E/W and corner halo buffers; the worst rank decides.
+    const int ranks = std::max(gpus, env_i("WORLD_SIZE", 1));
+    const Cart cart(ranks, P.decomp, P.px, P.py, P.nx, P.ny);
+    const int depth = P.tb_depth > 0 ? P.tb_depth : 12;
+    const int m = ranks > 1 ? (P.halo_passes > 0 ? P.halo_passes : 8) : 1;
+    int64_t worst = 0, worst_rank = 0;
+    for (int r = 0; r < ranks; ++r) {
+      const Block b = make_block(cart, r, P.nx, P.ny);
+      int64_t h = int64_t(depth) * m;
+      if (cart.px > 1) h = std::min<int64_t>(h, b.lx);
+      if (cart.py > 1) h = std::min<int64_t>(h, b.ly);
+      const Layout L = Layout::make(b.lx, b.ly, int(std::max<int64_t>(1, h)));
+      int64_t bytes = 2 * L.bytes();
+      if (cart.py > 1) bytes += 4 * b.lx * h * 4;
+      if (cart.px > 1 && cart.py > 1) bytes += 8 * h * h * 4;
+      if (bytes > worst) worst = bytes, worst_rank = r;
+    }
+    std::printf("{\"nx\": %lld, \"ny\": %lld, \"ranks\": %d, \"process_grid\": \"%dx%d\", "
+                "\"bytes_per_gpu\": %lld, \"gb_per_gpu\": %.3f, \"worst_rank\": %lld, "
+                "\"fits_288gb\": %s}\n",
+                (long long)P.nx, (long long)P.ny, ranks, cart.px, cart.py, (long long)worst,
+                double(worst) / 1e9, (long long)worst_rank, worst < int64_t(288e9 * 0.95) ? "true" : "false");
+    return 0;
+  }
   const int world = env_i("WORLD_SIZE", 1), rank = env_i("RANK", 0);
   const int local_rank = env_i("LOCAL_RANK", rank);
   const char* maddr = std::getenv("MASTER_ADDR");

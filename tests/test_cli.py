@@ -175,3 +175,18 @@ def test_make_ref_variants_wrappers(tmp_path):
                        capture_output=True, text=True, timeout=300, env=dict(os.environ, NP="2"))
     assert p.returncode == 0, p.stderr[-3000:]
     assert "converged" in p.stdout
+
+
+def test_cli_memory_plan(tmp_path):
+    # --plan: per-GPU bytes of the worst rank without allocating anything
+    # (131072^2 = two 68.7 GB fields: one MI355X or 1/8 of it per GPU).
+    one = json.loads(heat(["--nx", "131072", "--ny", "131072", "--plan"], tmp_path).stdout)
+    eight = json.loads(heat(["--nx", "131072", "--ny", "131072", "--gpus", "8", "--plan"],
+                            tmp_path).stdout)
+    assert one["process_grid"] == "1x1" and one["fits_288gb"]
+    assert 2 * 131072 ** 2 * 4 < one["bytes_per_gpu"] < 1.01 * 2 * 131072 ** 2 * 4
+    assert eight["process_grid"] == "4x2" and eight["ranks"] == 8
+    assert eight["bytes_per_gpu"] < one["bytes_per_gpu"] / 7.5
+    huge = json.loads(heat(["--nx", "600000", "--ny", "600000", "--gpus", "8", "--plan"],
+                           tmp_path).stdout)
+    assert not huge["fits_288gb"]
