@@ -99,10 +99,16 @@ struct RowUpdate {
                // lane holds the boundary column
   __device__ __forceinline__ vecf operator()(const vecf& a, const vecf& b, const vecf& c,
                                              bool row_ok) const {
+    return apply(a, b, c, dpp_from_left(b[V - 1]), dpp_from_right(b[0]), row_ok);
+  }
+  // wl / er: the west neighbour of element 0 (lane l-1's last element) and
+  // the east neighbour of element V-1 (lane l+1's first), shifted by the caller.
+  __device__ __forceinline__ vecf apply(const vecf& a, const vecf& b, const vecf& c, float wl,
+                                        float er, bool row_ok) const {
     vecf r;
 #if HEAT_TB_PACKED
-    const float w = dpp_from_left(b.w);
-    const float e = dpp_from_right(b.x);
+    const float w = wl;
+    const float e = er;
     // Explicit pairs (x,y) and (z,w): v_pk_add_f32 / v_pk_fma_f32 on aligned
     // register pairs; the east+west sums are scalar adds (two of them fuse
     // the DPP lane shift) written straight into aligned pairs.
@@ -123,8 +129,8 @@ struct RowUpdate {
 #else
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float w = j == 0 ? dpp_from_left(b[V - 1]) : b[j - 1];
-      const float e = j == V - 1 ? dpp_from_right(b[0]) : b[j + 1];
+      const float w = j == 0 ? wl : b[j - 1];
+      const float e = j == V - 1 ? er : b[j + 1];
       // stencil() sums e + w; for the last element pass them swapped (fp add
       // commutes, bitwise identical) so the DPP value is the operand the
       // compiler folds into v_add_f32_dpp, as it does for the first element.
@@ -201,7 +207,9 @@ struct TbStream {
         unsigned v;
         while ((v = __hip_atomic_load(produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <= q)
           __builtin_amdgcn_s_sleep(1);
-        seen = v;
+        // Uniform (every lane read the same word): keeps the per-row test
+        // `q >= seen` on the scalar unit instead of a VALU compare + branch.
+        seen = __builtin_amdgcn_readfirstlane(v);
       }
       asm volatile("" ::: "memory");
       const vecf x = ring[(q % kSplitRing) * 64 + (threadIdx.x & 63)];
@@ -215,18 +223,21 @@ struct TbStream {
     }
   }
 
+  // FAST: the caller guarantees rb <= ro < re (main-loop groups, see run())
+  // and passes ro * pitch as *woff (advanced here by one pitch).
+  template <bool FAST = false>
   __device__ __forceinline__ void emit(const vecf& out, const vecf& b, int64_t ro,
                                        float* __restrict__ dst, int64_t pitch, int64_t rb,
-                                       int64_t re, bool store_lane) {
+                                       int64_t re, bool store_lane, int64_t* woff = nullptr) {
     if constexpr (ROLE == 1) {
-      if (ro >= rb && ro < re) {  // every lane: stage 1 needs the overlap columns too
+      if (FAST || (ro >= rb && ro < re)) {  // every lane: stage 1 needs the overlap columns too
         const unsigned q = unsigned(ro - seq0);
         if (q >= seen + kSplitRing) {  // the slot's previous row may still be unread
           unsigned v;
           while ((v = __hip_atomic_load(released, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) +
                      kSplitRing <= q)
             __builtin_amdgcn_s_sleep(1);
-          seen = v;
+          seen = __builtin_amdgcn_readfirstlane(v);
         }
         asm volatile("" ::: "memory");
         ring[(q % kSplitRing) * 64 + (threadIdx.x & 63)] = out;
@@ -235,8 +246,13 @@ struct TbStream {
       }
       return;
     }
-    if (ro >= rb && ro < re && store_lane) {
-      if (!nostore) *reinterpret_cast<vecf*>(dst + ro * pitch) = out;
+    int64_t off = ro * pitch;
+    if constexpr (FAST) {
+      off = *woff;
+      *woff += pitch;
+    }
+    if ((FAST || (ro >= rb && ro < re)) && store_lane) {
+      if (!nostore) *reinterpret_cast<vecf*>(dst + off) = out;
       if constexpr (RES) {
         // Columns past the box end (the last lane's spill into padding or
         // stale ghost columns) are written but not part of the residual.
@@ -247,11 +263,15 @@ struct TbStream {
     }
   }
 
-  template <int U, int Q = U>
+  // FAST (LAG 3 main loop): the prefetched row i + PF needs no clamp and is
+  // read at src + roff (roff advanced by one pitch per row), and the output
+  // row needs no range test; see run().
+  template <int U, int Q = U, bool FAST = false>
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int rlo, int rhi,
-                                       bool store_lane, const RowUpdate<MODE>& upd) {
+                                       bool store_lane, const RowUpdate<MODE>& upd,
+                                       int64_t* roff = nullptr, int64_t* woff = nullptr) {
     if constexpr (LAG == 0) {
       // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
       // s holds rows i-s-2 (slot (U-s)&1) and i-s-1 (slot (U-s-1)&1).
@@ -274,24 +294,48 @@ struct TbStream {
       }
     } else {
       R[0][U] = P[Q];
-      P[Q] = load_row(src, min(i + PF, last_in), pitch);
+      if constexpr (FAST && ROLE != 2) {
+        P[Q] = *reinterpret_cast<const vecf*>(src + *roff);
+        *roff += pitch;
+      } else {
+        P[Q] = load_row(src, FAST ? i + PF : min(i + PF, last_in), pitch);
+      }
+#if HEAT_TB_BPERMUTE
+      // Every level's centre row (level s-1, row i - s) was produced in an
+      // earlier iteration: issue all 2K lane shifts (LDS crossbar round
+      // trips) up front so their latency overlaps, instead of each level
+      // waiting on its own pair (the scheduler otherwise places each pair
+      // just before its use in the stage-1 loop).
+      float wl[K + 1], er[K + 1];
+#pragma unroll
+      for (int s = 1; s <= K; ++s) {
+        const vecf& mid = R[s - 1][modn<RING>(U - STEP * s)];
+        wl[s] = dpp_from_left(mid[V - 1]);
+        er[s] = dpp_from_right(mid[0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd.apply(a_, b_, c_, wl[s], er[s], ok_)
+#else
+#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd(a_, b_, c_, ok_)
+#endif
       // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
       // iterations, so the order below carries no dependency.
 #pragma unroll
       for (int s = 1; s < K; ++s) {
         const int rs = STEP * s;  // this level's row is i - rs
         const bool ok = !ROWCHK || row_in(i - rs, rlo, rhi);
-        R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
-                                       R[s - 1][modn<RING>(U - rs)],
-                                       R[s - 1][modn<RING>(U - rs + 1)], ok);
+        R[s][modn<RING>(U - rs)] = HEAT_TB_UPD(s, R[s - 1][modn<RING>(U - rs - 1)],
+                                               R[s - 1][modn<RING>(U - rs)],
+                                               R[s - 1][modn<RING>(U - rs + 1)], ok);
       }
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
       const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
       const vecf& b = R[K - 1][modn<RING>(U - rK)];
-      const vecf out =
-          upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
-      emit(out, b, ro, dst, pitch, rb, re, store_lane);
+      const vecf out = HEAT_TB_UPD(K, R[K - 1][modn<RING>(U - rK - 1)], b,
+                                   R[K - 1][modn<RING>(U - rK + 1)], ok);
+#undef HEAT_TB_UPD
+      emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
     }
   }
 
@@ -365,7 +409,26 @@ struct TbStream {
       // region per iteration (keeps register pressure at the loop's level).
       ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
       constexpr int U0 = (2 * K) % 3;
-      for (int64_t t = 2 * K; t < T; t += 3) {
+      int64_t t = 2 * K;
+      // Main-loop groups (t, t+1, t+2) with t + 2 + PF <= last_in - first_in
+      // (= T - 1): every prefetch is an in-range row and every output row
+      // i - K = rb - 2K + t lies in [rb, re), so the group needs neither the
+      // clamp nor the range tests (their 64-bit compares are VALU work and
+      // VALU->branch stalls on gfx950).  The last <= PF + 2 iterations run
+      // the checked bodies below.
+      if (!cached_rows) {
+        int64_t roff = (first_in + t + PF) * pitch, woff = (first_in + t - K) * pitch;
+        for (; t + 3 + PF <= T; t += 3) {
+          const int64_t i = first_in + t;
+          body<U0, U0, true>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
+                             &roff, &woff);
+          body<(U0 + 1) % 3, (U0 + 1) % 3, true>(i + 1, t + 1, src, dst, pitch, last_in, rb, re,
+                                                 rlo, rhi, store_lane, upd, &roff, &woff);
+          body<(U0 + 2) % 3, (U0 + 2) % 3, true>(i + 2, t + 2, src, dst, pitch, last_in, rb, re,
+                                                 rlo, rhi, store_lane, upd, &roff, &woff);
+        }
+      }
+      for (; t < T; t += 3) {
         const int64_t i = first_in + t;
         body<U0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
         body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,

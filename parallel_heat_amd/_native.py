@@ -26,7 +26,8 @@ ABI_VERSION = 2  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
-LIB_PATH = PKG_DIR / "_lib" / "libheat.so"
+# HEAT_LIB: another build of the engine (kernel A/B timing in one tree).
+LIB_PATH = Path(os.environ["HEAT_LIB"]) if os.environ.get("HEAT_LIB") else PKG_DIR / "_lib" / "libheat.so"
 CLI_PATH = REPO_DIR / "build" / "heat"
 
 _lock = threading.Lock()
