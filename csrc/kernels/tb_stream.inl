@@ -174,14 +174,20 @@ struct TbStream {
   static constexpr bool ROWCHK = MODE == kModeGeneric;
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
   static constexpr int RING = LAG == 0 ? 2 : (LAG == 2 ? 4 : 3);
-  // Prefetch distance in rows (LAG 4 = LAG 3 with a 6-row prefetch ring).
-  static constexpr int PF = LAG == 4 ? 6 : RING;
+  // Prefetch distance in rows (LAG 3: part of the 6-row level-0 ring L0).
+  static constexpr int PF = RING;
   static constexpr int SKEW = LAG == 2 ? 2 : 1;
   static constexpr int STEP = LAG == 2 ? 2 : 1;  // row skew per level in the ring bodies
-  vecf R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows)
-  vecf P[PF];       // prefetch ring (input row i + PF)
+  vecf R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows; LAG 3: s >= 1)
+  vecf P[PF];       // prefetch ring (input row i + PF; LAG 0-2)
+  vecf L0[LAG == 3 ? 6 : 1];  // LAG 3: level-0 rows t-2 .. t+3 (see lv())
   unsigned m = 0;
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
+  // src / dst (run() arguments) point at the strip's first column, the same
+  // for every lane (scalar registers); lane l adds lo = V * l elements, so
+  // loads and stores use the scalar-base + 32-bit lane-offset addressing
+  // and the row arithmetic stays on the scalar unit.
+  int lo = 0;
   bool nostore = false;  // diagnostics only (kTbDiagNoStore): timing without the stores
   bool cached_rows = false;  // diagnostics only (kTbDiagCachedRows): loads hit 4 rows
 
@@ -219,7 +225,7 @@ struct TbStream {
       return x;
     } else {
       if (cached_rows) row = seq0 + (row & 3);  // diagnostics: cache-resident input
-      return *reinterpret_cast<const vecf*>(src + row * pitch);
+      return *reinterpret_cast<const vecf*>(src + row * pitch + lo);
     }
   }
 
@@ -252,7 +258,7 @@ struct TbStream {
       *woff += pitch;
     }
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
-      if (!nostore) *reinterpret_cast<vecf*>(dst + off) = out;
+      if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
       if constexpr (RES) {
         // Columns past the box end (the last lane's spill into padding or
         // stale ghost columns) are written but not part of the residual.
@@ -263,27 +269,22 @@ struct TbStream {
     }
   }
 
-  // FAST (LAG 3 main loop): the prefetched row i + PF needs no clamp and is
-  // read at src + roff (roff advanced by one pitch per row), and the output
-  // row needs no range test; see run().
-  template <int U, int Q = U, bool FAST = false>
+  // LAG 0 / 1 / 2 iteration (the LAG 3 pipelines use body3).
+  template <int U, int Q = U>
   __device__ __forceinline__ void body(int64_t i, int64_t t, const float* __restrict__ src,
                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
                                        int64_t rb, int64_t re, int rlo, int rhi,
-                                       bool store_lane, const RowUpdate<MODE>& upd,
-                                       int64_t* roff = nullptr, int64_t* woff = nullptr) {
+                                       bool store_lane, const RowUpdate<MODE>& upd) {
     if constexpr (LAG == 0) {
       // Slot of row r of level s: (r - first_in) mod 2.  At iteration i level
       // s holds rows i-s-2 (slot (U-s)&1) and i-s-1 (slot (U-s-1)&1).
       vecf c = P[U];
       {
         const int64_t nxt = min(i + RING, last_in);
-        P[U] = *reinterpret_cast<const vecf*>(src + nxt * pitch);
+        P[U] = *reinterpret_cast<const vecf*>(src + nxt * pitch + lo);
       }
 #pragma unroll
       for (int s = 0; s < K; ++s) {
-        constexpr int dummy = 0;
-        (void)dummy;
         const int sa = modn<2>(U - s), sb = modn<2>(U - s - 1);
         const int64_t row = i - s - 1;  // row of level s+1 computed now
         const bool ok = !ROWCHK || row_in(row, rlo, rhi);
@@ -294,49 +295,85 @@ struct TbStream {
       }
     } else {
       R[0][U] = P[Q];
-      if constexpr (FAST && ROLE != 2) {
-        P[Q] = *reinterpret_cast<const vecf*>(src + *roff);
-        *roff += pitch;
-      } else {
-        P[Q] = load_row(src, FAST ? i + PF : min(i + PF, last_in), pitch);
-      }
-#if HEAT_TB_BPERMUTE
-      // Every level's centre row (level s-1, row i - s) was produced in an
-      // earlier iteration: issue all 2K lane shifts (LDS crossbar round
-      // trips) up front so their latency overlaps, instead of each level
-      // waiting on its own pair (the scheduler otherwise places each pair
-      // just before its use in the stage-1 loop).
-      float wl[K + 1], er[K + 1];
-#pragma unroll
-      for (int s = 1; s <= K; ++s) {
-        const vecf& mid = R[s - 1][modn<RING>(U - STEP * s)];
-        wl[s] = dpp_from_left(mid[V - 1]);
-        er[s] = dpp_from_right(mid[0]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd.apply(a_, b_, c_, wl[s], er[s], ok_)
-#else
-#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd(a_, b_, c_, ok_)
-#endif
+      P[Q] = load_row(src, min(i + PF, last_in), pitch);
       // Levels 1..K-1.  With LAG 2 each reads only slots written in earlier
       // iterations, so the order below carries no dependency.
 #pragma unroll
       for (int s = 1; s < K; ++s) {
         const int rs = STEP * s;  // this level's row is i - rs
         const bool ok = !ROWCHK || row_in(i - rs, rlo, rhi);
-        R[s][modn<RING>(U - rs)] = HEAT_TB_UPD(s, R[s - 1][modn<RING>(U - rs - 1)],
-                                               R[s - 1][modn<RING>(U - rs)],
-                                               R[s - 1][modn<RING>(U - rs + 1)], ok);
+        R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
+                                       R[s - 1][modn<RING>(U - rs)],
+                                       R[s - 1][modn<RING>(U - rs + 1)], ok);
       }
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
       const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
       const vecf& b = R[K - 1][modn<RING>(U - rK)];
-      const vecf out = HEAT_TB_UPD(K, R[K - 1][modn<RING>(U - rK - 1)], b,
-                                   R[K - 1][modn<RING>(U - rK + 1)], ok);
-#undef HEAT_TB_UPD
-      emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
+      const vecf out =
+          upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
+      emit(out, b, ro, dst, pitch, rb, re, store_lane);
     }
+  }
+
+  // LAG 3 rows, by iteration t (input row first_in + t): level 0 row t + d
+  // is L0[(t + d) mod 6] -- the three rows level 1 reads plus the three
+  // prefetched ones, one ring, so no row is ever copied from a prefetch
+  // buffer into the level-0 ring (with separate rings the register
+  // allocator rotated them with moves at the loop back-edge, which waited
+  // for the row loaded in that same iteration: vmcnt(0) every 3 rows);
+  // level s > 0 row t + d is R[s][(t + d) mod 3].  s and d fold to
+  // constants once the level loops are unrolled.
+  __device__ __forceinline__ vecf& lv(int s, int td) {
+    return s == 0 ? L0[modn<6>(td)] : R[s][modn<3>(td)];
+  }
+
+  // One LAG 3 iteration, t = T6 (mod 6).  FAST (main-loop groups, see run()):
+  // the prefetched row needs no clamp and is read at src + *roff, the output
+  // row needs no range test and is written at dst + *woff (both advanced by
+  // one pitch per row).
+  template <int T6, bool FAST>
+  __device__ __forceinline__ void body3(int64_t i, const float* __restrict__ src,
+                                        float* __restrict__ dst, int64_t pitch, int64_t last_in,
+                                        int64_t rb, int64_t re, int rlo, int rhi,
+                                        bool store_lane, const RowUpdate<MODE>& upd,
+                                        int64_t* roff, int64_t* woff) {
+    // Row t + 3 into the slot of row t - 3 (level 1 now reads t-2 .. t).
+    if constexpr (FAST && ROLE != 2) {
+      L0[modn<6>(T6 + 3)] = *reinterpret_cast<const vecf*>(src + *roff + lo);
+      *roff += pitch;
+    } else {
+      L0[modn<6>(T6 + 3)] = load_row(src, FAST ? i + 3 : min(i + 3, last_in), pitch);
+    }
+#if HEAT_TB_BPERMUTE
+    // Every level's centre row (level s-1, row t - s) was produced in an
+    // earlier iteration: issue all 2K lane shifts (LDS crossbar round trips)
+    // up front so their latencies overlap, instead of each level waiting on
+    // its own pair (where the scheduler otherwise puts them in stage 1).
+    float wl[K + 1], er[K + 1];
+#pragma unroll
+    for (int s = 1; s <= K; ++s) {
+      const vecf& mid = lv(s - 1, T6 - s);
+      wl[s] = dpp_from_left(mid[V - 1]);
+      er[s] = dpp_from_right(mid[0]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd.apply(a_, b_, c_, wl[s], er[s], ok_)
+#else
+#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd(a_, b_, c_, ok_)
+#endif
+#pragma unroll
+    for (int s = 1; s < K; ++s) {  // level s computes row t - s
+      const bool ok = !ROWCHK || row_in(i - s, rlo, rhi);
+      lv(s, T6 - s) = HEAT_TB_UPD(s, lv(s - 1, T6 - s - 1), lv(s - 1, T6 - s),
+                                  lv(s - 1, T6 - s + 1), ok);
+    }
+    const int64_t ro = i - K;  // output row of this iteration
+    const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
+    const vecf& b = lv(K - 1, T6 - K);
+    const vecf out = HEAT_TB_UPD(K, lv(K - 1, T6 - K - 1), b, lv(K - 1, T6 - K + 1), ok);
+#undef HEAT_TB_UPD
+    emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
   }
 
   template <int T, int S>
@@ -345,8 +382,7 @@ struct TbStream {
     if constexpr (S < K) {
       if constexpr (2 * S <= T) {
         const bool ok = !ROWCHK || row_in(i - S, rlo, rhi);
-        R[S][modn<3>(T - S)] = upd(R[S - 1][modn<3>(T - S - 1)], R[S - 1][modn<3>(T - S)],
-                                   R[S - 1][modn<3>(T - S + 1)], ok);
+        lv(S, T - S) = upd(lv(S - 1, T - S - 1), lv(S - 1, T - S), lv(S - 1, T - S + 1), ok);
       }
       ramp_levels<T, S + 1>(i, rlo, rhi, upd);
     }
@@ -356,10 +392,8 @@ struct TbStream {
                                        int64_t pitch, int64_t last_in, int rlo, int rhi,
                                        const RowUpdate<MODE>& upd) {
     if constexpr (T < 2 * K) {
-      constexpr int U = T % 3, Q = T % PF;
       const int64_t i = first_in + T;
-      R[0][U] = P[Q];
-      P[Q] = load_row(src, min(i + PF, last_in), pitch);
+      L0[modn<6>(T + 3)] = load_row(src, min(i + 3, last_in), pitch);
       ramp_levels<T, 1>(i, rlo, rhi, upd);
       __builtin_amdgcn_sched_barrier(0);
       ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
@@ -369,7 +403,8 @@ struct TbStream {
   __device__ __forceinline__ void run(const float* __restrict__ src, float* __restrict__ dst,
                                       int64_t pitch, int64_t rb, int64_t re, int rlo, int rhi,
                                       bool store_lane, const RowUpdate<MODE>& upd) {
-    // src/dst are offset to this lane's column; rows are local rows.
+    // src/dst point at the strip's first column (+ lo for this lane); rows
+    // are local rows.
     const int64_t first_in = rb - K, last_in = re + K - 1;
     // The last output row (re-1) leaves the pipeline at iteration re-1+SKEW*K.
     const int64_t T = (re - 1 + SKEW * K) - first_in + 1;
@@ -378,66 +413,66 @@ struct TbStream {
 #pragma unroll
       for (int j = 0; j < RING; ++j) R[s][j] = vecf(0.f);
     if constexpr (ROLE != 1) seq0 = first_in;
-#pragma unroll
-    for (int j = 0; j < PF; ++j) P[j] = load_row(src, min(first_in + j, last_in), pitch);
-    if constexpr (LAG == 4) {
-      // As LAG 3, with the main loop unrolled by 6 for the 6-row prefetch ring.
-      ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
-      constexpr int T0 = 2 * K;
-      for (int64_t t = T0; t < T; t += 6) {
-        const int64_t i = first_in + t;
-        body<(T0 + 0) % 3, (T0 + 0) % 6>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi,
-                                         store_lane, upd);
-        body<(T0 + 1) % 3, (T0 + 1) % 6>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd);
-        body<(T0 + 2) % 3, (T0 + 2) % 6>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd);
-        body<(T0 + 3) % 3, (T0 + 3) % 6>(i + 3, t + 3, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd);
-        body<(T0 + 4) % 3, (T0 + 4) % 6>(i + 4, t + 4, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd);
-        body<(T0 + 5) % 3, (T0 + 5) % 6>(i + 5, t + 5, src, dst, pitch, last_in, rb, re, rlo,
-                                         rhi, store_lane, upd);
-      }
-      return;
-    }
     if constexpr (LAG == 3) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        L0[j] = j < 3 ? load_row(src, min(first_in + j, last_in), pitch) : vecf(0.f);
       // Pipeline ramp: during iteration t < 2K only levels s <= t/2 compute
       // rows the chunk's output trapezoid needs; a plain loop would compute
       // 2s useless rows per level per chunk (a third of all work for short
       // chunks).  The ramp is unrolled at compile time, one scheduling
       // region per iteration (keeps register pressure at the loop's level).
       ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
-      constexpr int U0 = (2 * K) % 3;
-      int64_t t = 2 * K;
-      // Main-loop groups (t, t+1, t+2) with t + 2 + PF <= last_in - first_in
+      constexpr int T0 = 2 * K;
+      int64_t t = T0;
+      // Main-loop groups t .. t+5 with t + 5 + 3 <= last_in - first_in
       // (= T - 1): every prefetch is an in-range row and every output row
-      // i - K = rb - 2K + t lies in [rb, re), so the group needs neither the
-      // clamp nor the range tests (their 64-bit compares are VALU work and
-      // VALU->branch stalls on gfx950).  The last <= PF + 2 iterations run
-      // the checked bodies below.
+      // first_in + t - K (>= rb from t = 2K on) lies below re, so the group
+      // needs neither the clamp nor the range tests (64-bit compares are
+      // VALU work plus VALU->branch stalls on gfx950).  The last < 9
+      // iterations run checked bodies.
       if (!cached_rows) {
-        int64_t roff = (first_in + t + PF) * pitch, woff = (first_in + t - K) * pitch;
-        for (; t + 3 + PF <= T; t += 3) {
+        int64_t roff = (first_in + t + 3) * pitch, woff = (first_in + t - K) * pitch;
+        for (; t + 9 <= T; t += 6) {
           const int64_t i = first_in + t;
-          body<U0, U0, true>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd,
-                             &roff, &woff);
-          body<(U0 + 1) % 3, (U0 + 1) % 3, true>(i + 1, t + 1, src, dst, pitch, last_in, rb, re,
-                                                 rlo, rhi, store_lane, upd, &roff, &woff);
-          body<(U0 + 2) % 3, (U0 + 2) % 3, true>(i + 2, t + 2, src, dst, pitch, last_in, rb, re,
-                                                 rlo, rhi, store_lane, upd, &roff, &woff);
+          body3<(T0 + 0) % 6, true>(i, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
+                                    upd, &roff, &woff);
+          body3<(T0 + 1) % 6, true>(i + 1, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                    store_lane, upd, &roff, &woff);
+          body3<(T0 + 2) % 6, true>(i + 2, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                    store_lane, upd, &roff, &woff);
+          body3<(T0 + 3) % 6, true>(i + 3, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                    store_lane, upd, &roff, &woff);
+          body3<(T0 + 4) % 6, true>(i + 4, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                    store_lane, upd, &roff, &woff);
+          body3<(T0 + 5) % 6, true>(i + 5, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                    store_lane, upd, &roff, &woff);
         }
       }
-      for (; t < T; t += 3) {
+      for (; t < T; t += 6) {
         const int64_t i = first_in + t;
-        body<U0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
-        body<(U0 + 1) % 3>(i + 1, t + 1, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
-                           upd);
-        body<(U0 + 2) % 3>(i + 2, t + 2, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
-                           upd);
+        body3<(T0 + 0) % 6, false>(i, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane,
+                                   upd, nullptr, nullptr);
+        if (t + 1 >= T) break;
+        body3<(T0 + 1) % 6, false>(i + 1, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                   store_lane, upd, nullptr, nullptr);
+        if (t + 2 >= T) break;
+        body3<(T0 + 2) % 6, false>(i + 2, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                   store_lane, upd, nullptr, nullptr);
+        if (t + 3 >= T) break;
+        body3<(T0 + 3) % 6, false>(i + 3, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                   store_lane, upd, nullptr, nullptr);
+        if (t + 4 >= T) break;
+        body3<(T0 + 4) % 6, false>(i + 4, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                   store_lane, upd, nullptr, nullptr);
+        if (t + 5 >= T) break;
+        body3<(T0 + 5) % 6, false>(i + 5, src, dst, pitch, last_in, rb, re, rlo, rhi,
+                                   store_lane, upd, nullptr, nullptr);
       }
       return;
     }
+#pragma unroll
+    for (int j = 0; j < PF; ++j) P[j] = load_row(src, min(first_in + j, last_in), pitch);
     for (int64_t t = 0; t < T; t += RING) {
       const int64_t i = first_in + t;
       body<0>(i, t, src, dst, pitch, last_in, rb, re, rlo, rhi, store_lane, upd);
@@ -457,7 +492,6 @@ constexpr int tb_waves_per_simd() {
   // float2 lanes: half the ring registers.
   if (V == 2) return K <= 4 ? 8 : K <= 6 ? 6 : 5;
   if (LAG == 2) return K <= 4 ? 4 : 2;
-  if (LAG == 4) return K <= 2 ? 6 : K <= 4 ? 4 : K <= 6 ? 3 : K <= 8 ? 3 : 2;
   return K <= 2 ? 6 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 8 ? 3 : 2;
 }
 
@@ -522,8 +556,8 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
   }
 
   const StencilGeom& g = a.g;
-  const float* src = a.src + col;
-  float* dst = a.dst + col;
+  const float* src = a.src + (cbase - KK);  // wave-uniform; + lo per lane
+  float* dst = a.dst + (cbase - KK);
   int64_t pitch = g.pitch;
   const bool want_resid = a.resid != nullptr;
 
@@ -569,6 +603,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
     }
     if constexpr (K1 == 0) {
       TbStream<K, LAG, MD, decltype(res_c)::value> st;
+      st.lo = V * lane;
       st.rc = int(min<int64_t>(cend - col, V));
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
@@ -577,6 +612,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
     } else if (stage == 0) {
       // Level-K1 rows [rb - K2, re + K2): exactly what stage 1's trapezoid reads.
       TbStream<K1, LAG, MD, false, 1> st;
+      st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
@@ -585,6 +621,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
     } else {
       TbStream<K2, LAG, MD, decltype(res_c)::value, 2> st;
+      st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
@@ -717,10 +754,10 @@ int occupancy(int depth, int lag) {
   }
 }
 
-// Returns false if (depth, lag) is not instantiated.  LAG 4 (6-row prefetch)
-// measured equal to LAG 3 (profiles/tb_depth_bandwidth_calibration_r1.jsonl:
-// K=8 already moves ~4.4 TB/s of the ~4.9 TB/s this access pattern reaches)
-// and is not instantiated either.  Only the skew-1
+// Returns false if (depth, lag) is not instantiated.  A 6-row prefetch (the
+// round-1 "LAG 4") measured equal to LAG 3's 3 rows
+// (profiles/tb_depth_bandwidth_calibration_r1.jsonl: K=8 already moves
+// ~4.4 TB/s of the ~4.9 TB/s this access pattern reaches) and was removed.  Only the skew-1
 // pipelines (LAG 1, and LAG 3 = LAG 1 + ramp) are instantiated: the skew-2
 // (LAG 2) and 2-slot (LAG 0) forms lost every sweep (profiles/tb_sweep_*.json)
 // and only cost build time.
