@@ -455,11 +455,14 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   const int64_t min_len = ml && *ml ? std::max(1, std::atoi(ml)) : std::max<int64_t>(depth, 8);
   int64_t len = std::max<int64_t>(min_len, ceil_div(total_strip_rows, waves_target));
   // Rows whose chunk window reaches the global top/bottom row run the
-  // generic (masked) path, which is slower: give them shorter chunks, as
-  // separate sub-boxes, so those waves do not set the tail of the launch.
+  // generic (masked) path: HEAT_TB_EDGE_FRAC < 1 gives them shorter chunks,
+  // as separate sub-boxes.  Default 1 (no edge sub-boxes) since the round-2
+  // main loop: the edge chunks at 0.75 finished ~30 us before the rest of an
+  // 8192^2 launch; bench.py 1.0 vs 0.95 / 0.9 / 0.75: +0.4 / +1.2 / +1.2 %
+  // (profiles/tb_edge_frac_r2.md).
   static const double edge_frac = [] {
     const char* e = std::getenv("HEAT_TB_EDGE_FRAC");
-    return e && *e ? std::atof(e) : 0.75;
+    return e && *e ? std::atof(e) : 1.0;
   }();
   int n = 0, waves = 0;
   auto plan = [&](int64_t L) {
@@ -491,23 +494,30 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       const Box& B = boxes[b];
       if (B.empty()) continue;
       HEAT_CHECK(B.c0 % 4 == 0, "TB box column start %lld not a multiple of 4", (long long)B.c0);
-      Box mid = B;
+      Box mid = B, top{}, bot{};
       if (edge_len < L && B.rows() > 2 * L) {
         // Local rows whose window [r - depth, r + depth] touches global row 0 / nx-1.
         const int64_t top_end = 1 - g.gx0 + depth;          // first row clear of the top
         const int64_t bot_begin = g.nx - 2 - g.gx0 - depth;  // last row clear of the bottom
         if (B.r0 < top_end) {
           const int64_t e = std::min(B.r1, std::max(top_end, B.r0 + edge_len));
-          add(Box{B.r0, e, B.c0, B.c1}, edge_len);
+          top = Box{B.r0, e, B.c0, B.c1};
           mid.r0 = e;
         }
         if (B.r1 - 1 > bot_begin && mid.r1 > mid.r0) {
           const int64_t s0 = std::max(mid.r0, std::min(bot_begin + 1, B.r1 - edge_len));
-          add(Box{s0, B.r1, B.c0, B.c1}, edge_len);
+          bot = Box{s0, B.r1, B.c0, B.c1};
           mid.r1 = s0;
         }
       }
+      // Units in plate order (top edge, middle, bottom edge): XCD groups
+      // take contiguous unit ranges, so the short edge units land on the
+      // first and the last XCD instead of all on the first (which then
+      // idled for the last ~15 % of the launch, tools/wave_timeline.py
+      // xcd_last_end_us).
+      add(top, edge_len);
       add(mid, L);
+      add(bot, edge_len);
     }
   };
   // Keep the total within waves_target (whole resident rounds): a few extra

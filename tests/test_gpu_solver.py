@@ -142,3 +142,28 @@ def test_gpu_mpi_numerics(gpu):
     assert np.array_equal(g, ref)
     with pytest.raises(Exception, match="naive"):
         HeatSolver(cfg.replace(kernel="tb"))
+
+
+@pytest.mark.parametrize("edge_frac", ["0.75", "0.5"])
+def test_tb_edge_subboxes_bitwise(gpu, tmp_path, edge_frac):
+    # HEAT_TB_EDGE_FRAC < 1 plans the plate's top/bottom chunks as separate
+    # shorter sub-boxes (off by default since the round-2 edge A/B,
+    # profiles/tb_edge_frac_r2.md).  The planner reads it once per process,
+    # so run the CLI with it and compare with the CPU oracle's checksum.
+    import json
+    import os
+    import subprocess
+
+    from parallel_heat_amd import _native
+    # Tall enough that chunks are longer than the minimum (edge boxes exist).
+    args = ["--nx", "8192", "--ny", "1000", "--steps", "30", "--init", "random",
+            "--out", "c.json", "--out-format", "checksum"]
+    got = {}
+    for backend in ("hip", "cpu"):
+        d = tmp_path / backend
+        d.mkdir()
+        env = dict(os.environ, HEAT_TB_EDGE_FRAC=edge_frac)
+        subprocess.run([str(_native.CLI_PATH), "--backend", backend] + args, cwd=d, env=env,
+                       capture_output=True, text=True, timeout=300, check=True)
+        got[backend] = json.loads((d / "c.json").read_text())
+    assert got["hip"]["hash"] == got["cpu"]["hash"]
