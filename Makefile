@@ -24,16 +24,21 @@ OBJS     := $(patsubst csrc/src/%.cpp,$(BUILD)/obj/%.o,$(SRCS_CPP)) \
 
 all: $(LIBDIR)/libheat.so $(BUILD)/heat
 
-$(BUILD)/obj/%.o: csrc/src/%.cpp $(HDRS)
+# Header dependencies come from the compiler (-MMD): a header edit rebuilds
+# only the objects that include it (the TB kernel builds take minutes each).
+DEPFLAGS = -MMD -MP
+$(BUILD)/obj/%.o: csrc/src/%.cpp
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -x hip -c $< -o $@
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
 $(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o: HIPFLAGS += -fno-slp-vectorize
 
-$(BUILD)/obj/%.o: csrc/kernels/%.hip $(HDRS) $(KHDRS)
+$(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -c $< -o $@
+
+-include $(OBJS:.o=.d)
 
 $(LIBDIR)/libheat.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
@@ -46,10 +51,14 @@ probe: $(BUILD)/overlap_probe
 $(BUILD)/overlap_probe: tools/overlap_probe.cpp $(OBJS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip tools/overlap_probe.cpp -x none $(OBJS) -o $@ $(LDFLAGS)
 
-asm: $(SRCS_HIP)
+# One kernel source at a time (ASM=tb_split), with the same per-file flags as
+# the object build: the TB builds take ~10 minutes each.
+ASM ?= tb_split
+asm:
 	@mkdir -p $(BUILD)/asm
-	cd $(BUILD)/asm && for f in $(SRCS_HIP); do \
-	  $(HIPCC) $(patsubst -Icsrc/include,-I../../csrc/include,$(HIPFLAGS)) --offload-device-only -S -o $$(basename $$f .hip).s ../../$$f; done
+	cd $(BUILD)/asm && $(HIPCC) $(patsubst -Icsrc/include,-I../../csrc/include,$(HIPFLAGS)) \
+	  $(if $(filter tb_scalar tb_split,$(ASM)),-fno-slp-vectorize) --offload-device-only -S \
+	  -o $(ASM).s ../../csrc/kernels/$(ASM).hip
 
 resources: $(SRCS_HIP)
 	$(HIPCC) $(HIPFLAGS) -c csrc/kernels/stencil.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \

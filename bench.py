@@ -45,7 +45,9 @@ import argparse
 import faulthandler
 import json
 import os
+import re
 import sys
+import tempfile
 import time
 
 import torch
@@ -57,6 +59,24 @@ METRIC = "Mcells/sec (whole node) + sec/1000 iters, 8192^2 grid at 1/2/4/8 MI355
 
 def log(rank: int, msg: str) -> None:
     print(f"[bench] rank {rank}: {msg}", file=sys.stderr, flush=True)
+
+
+_LINK = re.compile(r"(\d+)\[[^\]]*\] -> (\d+)\[[^\]]*\] (?:\[\w+\] )?via (\S+)")
+
+
+def rccl_links(path: str) -> list:
+    """Distinct 'src->dst via TRANSPORT' channel connections RCCL logged
+    (NCCL_DEBUG=INFO, subsystems INIT,P2P) for this rank's communicators."""
+    seen = set()
+    try:
+        with open(path, errors="replace") as f:
+            for line in f:
+                m = _LINK.search(line)
+                if m:
+                    seen.add(f"{m.group(1)}->{m.group(2)} via {m.group(3)}")
+    except OSError:
+        return []
+    return sorted(seen)
 
 
 def main() -> int:
@@ -73,8 +93,14 @@ def main() -> int:
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--decomp", default="rows")
     ap.add_argument("--converge", action="store_true",
-                    help="also run the convergence check (never converges on random data)")
+                    help="also run the convergence check every --check-interval steps (a run "
+                         "stops at its converging check; random data converges within a few "
+                         "hundred steps, --init ref-wrap does not within a bench run)")
     ap.add_argument("--check-interval", type=int, default=50)
+    ap.add_argument("--eps", type=float, default=1e-3)
+    ap.add_argument("--init", default="random",
+                    help="initial condition: random (synthetic, default) | ref-wrap (the "
+                         "reference's inidat, int32-wrapped)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--verbose", action="store_true")
@@ -120,8 +146,16 @@ def main() -> int:
     watchdog("init", args.watchdog_s)
     device = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(device)
+    rccl_log = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "NCCL_DEBUG" not in os.environ:
+            # Record which transport RCCL picks for each neighbour pair (xGMI
+            # P2P on a node) in a per-rank file, reported in the JSON line.
+            rccl_log = os.path.join(tempfile.gettempdir(),
+                                    f"heat_rccl_{os.getpid()}_r{rank}.log")
+            os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P",
+                              NCCL_DEBUG_FILE=rccl_log)
         if os.environ.get("HEAT_RCCL_HOST_PER_RANK") == "1":
             # Rehearsal hook for a 1-GPU box (tools/rccl_rehearsal.sh): RCCL
             # refuses two ranks on one device of one host, so each rank claims
@@ -134,14 +168,45 @@ def main() -> int:
     from parallel_heat_amd import HeatConfig, HeatSolver, _native
     from parallel_heat_amd.parallel.comm import DistInfo
 
-    cfg = HeatConfig(nx=args.nx, ny=args.ny, steps=args.iters_per_step, init="random", seed=1234,
+    cfg = HeatConfig(nx=args.nx, ny=args.ny, steps=args.iters_per_step, init=args.init, seed=1234,
                      backend="hip", kernel=args.kernel, tb_depth=args.tb_depth,
                      decomp=args.decomp, converge=args.converge,
-                     check_interval=args.check_interval, use_graph=not args.no_graph,
+                     check_interval=args.check_interval, eps=args.eps,
+                     use_graph=not args.no_graph,
                      overlap=not args.no_overlap, device=device,
                      schedule=args.schedule, halo_passes=args.halo_passes,
                      phase_timing=args.phase_timing)
     info = DistInfo(rank, world, local_rank)
+
+    def vote(ok: bool) -> bool:
+        """True on every rank iff ok on every rank (torch's own group)."""
+        if world == 1:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    # ONE engine transport per rank for the whole run: the autotune
+    # candidates and the benchmarked solver all use this RCCL communicator.
+    shared = None
+    if world > 1:
+        from parallel_heat_amd.parallel.comm import EngineTransport
+        err = None
+        try:
+            shared = EngineTransport("rccl", info, device=device)
+        except _native.NativeError as e:
+            err = e
+        if not vote(shared is not None):
+            log(rank, f"RCCL transport failed on some rank ({err})")
+            if shared is not None:
+                shared.close()
+                shared = None
+            if not args.allow_fallback:
+                log(rank, "RCCL transport unavailable on some rank; exiting "
+                          "(--allow-fallback runs host-staged halos over gloo instead)")
+                return 1
+            log(rank, "falling back to host-staged halos over gloo (all ranks)")
+            shared = EngineTransport("torch", info, group=dist.new_group(backend="gloo"))
 
     tuning = None
     if world > 1 and not args.no_autotune:
@@ -156,36 +221,24 @@ def main() -> int:
                                    halo_passes=[int(x) for x in
                                                 args.autotune_halo_passes.split(",") if x])
         try:
-            cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=2,
-                                   log=(lambda m: log(rank, m)) if args.verbose else None)
+            cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=3,
+                                   log=(lambda m: log(rank, m)) if args.verbose else None,
+                                   shared=shared)
         except _native.NativeError as e:
-            # e.g. RCCL unavailable: the transport vote below decides.
+            # Every candidate rejected (the ranks agree inside autotune).
             log(rank, f"autotune failed ({e}); using --decomp {args.decomp}")
 
     solver = None
+    err = None
     try:
-        solver = HeatSolver(cfg, dist_info=info)
+        solver = HeatSolver(cfg, dist_info=info, shared=shared)
     except _native.NativeError as e:
         if world == 1:
             raise
-        log(rank, f"RCCL transport failed: {e}")
-    if world > 1:
-        # Every rank must agree on the transport before the first exchange:
-        # a rank whose communicator failed would otherwise leave its peers
-        # blocked in RCCL.  torch's own process group carries the vote.
-        ok = torch.tensor([1 if solver is not None else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            if solver is not None:
-                solver.close()
-                solver = None
-            if not args.allow_fallback:
-                log(rank, "RCCL transport unavailable on some rank; exiting "
-                          "(--allow-fallback runs host-staged halos over gloo instead)")
-                return 1
-            log(rank, "falling back to host-staged halos over gloo (all ranks)")
-            solver = HeatSolver(cfg, transport="torch", dist_info=info,
-                                group=dist.new_group(backend="gloo"))
+        err = e
+    if not vote(solver is not None):
+        log(rank, f"solver construction failed on some rank ({err})")
+        return 1
 
     def barrier():
         if world > 1:
@@ -217,6 +270,21 @@ def main() -> int:
     if not args.no_verify:
         watchdog("verify", args.watchdog_s)
         verified, check = verify(solver, cfg, rank, world, device, HeatSolver, DistInfo)
+    rccl = None
+    if shared is not None:
+        # What the engine's communicator saw, from every rank: its rank count
+        # and device (ncclCommCount / ncclCommCuDevice), the PCI bus id, and
+        # the transport RCCL logged for each channel connection.
+        mine = dict(shared.info(), rank=rank, local_rank=local_rank,
+                    links=rccl_links(rccl_log) if rccl_log else None)
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        links = sorted({l for r in every for l in (r.get("links") or [])})
+        rccl = {"transport": mine["name"], "nranks": mine["nranks"],
+                "ranks": [{k: r[k] for k in ("rank", "user_rank", "device", "bus_id")}
+                          for r in every],
+                "distinct_devices": len({r["bus_id"] or r["device"] for r in every}),
+                "links": links if rccl_log else "not recorded (NCCL_DEBUG set by the caller)"}
     faulthandler.cancel_dump_traceback_later()
 
     cells = args.nx * args.ny * done
@@ -236,7 +304,8 @@ def main() -> int:
             "scaling": "weak" if args.weak else "strong",
             "vs_baseline": round(mcells / BASELINE_MCELLS, 3),
             "dtype": "fp32",
-            "data": "synthetic (random-init temperature grid, seed 1234)",
+            "data": ("synthetic (random-init temperature grid, seed 1234)" if args.init == "random"
+                     else f"synthetic ({args.init} initial condition of the reference)"),
             "config": {
                 "model": "heat2d 5-point Jacobi (fixed boundary)",
                 "grid": f"{args.nx}x{args.ny}",
@@ -246,12 +315,15 @@ def main() -> int:
                 "parallelism": f"domain-decomp {solver.info.px}x{solver.info.py} "
                                f"({solver.transport}), tb_depth {solver.info.tb_depth}, "
                                f"halo {solver.info.halo}, schedule {solver.info.schedule}",
-                "converge_check": bool(args.converge),
+                "converge_check": (f"every {args.check_interval} steps, eps {args.eps:g}"
+                                   if args.converge else False),
             },
             "verified": verified,
         }
         if tuning is not None:
             line["autotune"] = tuning
+        if rccl is not None:
+            line["rccl"] = rccl
         if check:
             line["verification"] = check
         if args.verbose:
@@ -262,6 +334,8 @@ def main() -> int:
                                            "reduce": round(phases[2], 6)}
         print(json.dumps(line), flush=True)
     solver.close()
+    if shared is not None:
+        shared.close()
     if world > 1:
         dist.destroy_process_group()
     return 0 if verified is not False else 2

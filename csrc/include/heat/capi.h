@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define HEAT_ABI_VERSION 2
+#define HEAT_ABI_VERSION 3
 
 typedef struct heat_params {
   int64_t nx, ny;
@@ -84,6 +84,15 @@ typedef struct heat_checksum {
 } heat_checksum;
 
 typedef struct heat_solver heat_solver;
+typedef struct heat_transport heat_transport;
+
+typedef struct heat_transport_info {
+  int32_t nranks;      /* rccl: ncclCommCount; else the world size */
+  int32_t device;      /* rccl: ncclCommCuDevice; else -1 */
+  int32_t user_rank;   /* rccl: ncclCommUserRank; else the rank */
+  char bus_id[32];     /* PCI bus id of `device` ("" if unknown) */
+  char name[16];       /* transport name */
+} heat_transport_info;
 
 const char* heat_last_error(void);
 int heat_abi_version(void);
@@ -93,6 +102,12 @@ int heat_rccl_unique_id(uint8_t out[128]);
 int heat_device_count(int* n);
 
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out);
+/* A transport (e.g. one RCCL communicator) that several solvers use in turn:
+ * each solver keeps a reference, so destroying the handle early is safe. */
+int heat_transport_create(const heat_comm* c, heat_transport** out);
+int heat_transport_destroy(heat_transport* t);
+int heat_transport_info_get(heat_transport* t, heat_transport_info* out);
+int heat_solver_create_shared(const heat_params* p, heat_transport* t, heat_solver** out);
 int heat_solver_destroy(heat_solver* s);
 int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
 /* RCCL on one rank: self send/recv (eager or hipGraph-captured) + all-reduce. */
@@ -144,7 +159,17 @@ int heat_op_tb_stamps(void* buf, int64_t waves);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,
-                    int variant /* -1 default; bit0 lag-2, bit1 scalar build */);
+                    int variant /* -1 default; heat::gpu::tbv flags */,
+                    int res_level /* residual after this step of the pass; 0 = depth */);
+/* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares. */
+typedef struct heat_tb_tuning {
+  int32_t variant, rounds, min_len, waves;
+  double edge_frac;
+  int32_t n_weights, pad_;
+  double weights[4];
+} heat_tb_tuning;
+int heat_tb_get_tuning(heat_tb_tuning* out);
+int heat_tb_set_tuning(const heat_tb_tuning* in);
 int heat_op_init(float* origin, int64_t lx, int64_t ly, int halo, int64_t gx0, int64_t gy0,
                  int64_t nx, int64_t ny, int mode, uint64_t seed, void* stream);
 int heat_op_pack(const float* origin, int64_t pitch, int64_t r0, int64_t r1, int64_t c0,

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "heat/topology.hpp"
 
@@ -29,7 +30,37 @@ struct StencilGeom {
   int64_t nx = 0, ny = 0;
   float cx = 0.1f, cy = 0.1f;
   int numerics = 0;  // heat::Numerics (naive kernel only; TB is always Fp32)
+  // Convergence gate (device word, null = none): a launch whose gate reads
+  // non-zero writes nothing (see judge_check).
+  const unsigned* gate = nullptr;
 };
+
+// Variant flags of the temporally blocked kernel (tb_step's `variant`; the
+// same names in parallel_heat_amd.ops.TbVariant).  Bits 0-1 choose the
+// register pipeline, the rest the build and the launch layout.
+namespace tbv {
+enum : int {
+  kRing3 = 0,           // 3-row rings, skew 1 (LAG 1)
+  kRing4 = 1,           // 4-row rings, skew 2 (LAG 2)
+  kRing2 = 2,           // 2-row rings + copy (LAG 0)
+  kRamp = 3,            // 3-row rings + compile-time ramp skip (LAG 3)
+  kPipeMask = 3,
+  kScalar = 4,          // scalar row update build (tbs; depth 12 lives here)
+  kPrefetch6 = 8,       // with kRamp: 6-row prefetch (retired, LAG 4)
+  kXcdGroups = 16,      // contiguous wave ranges per XCD
+  kAltDirection = 32,   // odd chunks stream bottom-up
+  kFloat2 = 64,         // float2 lanes, 128-column strips (tbn)
+  kForceAgePairs = 256, // age groups even at equal weights (tests)
+  kDiagNoStore = 1024,  // diagnostics: no output stores (wrong results)
+  kSplit = 2048,        // two-wave level-split pipelines (tbx; depths 8, 12)
+  kDiagCachedRows = 4096,  // diagnostics: cache-resident input rows (wrong results)
+  kNoAgePairs = 16384,  // never age-group (A/B of the weights)
+  kLinear = 32768,      // balanced linear plan (equal strip-rows per unit)
+  // Defaults: depth <= 8 and small launches at 12; large launches at 12.
+  kDefault = kRamp | kScalar | kXcdGroups,  // 23
+  kDefaultDeep = kDefault | kSplit,         // 2071
+};
+}  // namespace tbv
 
 // Depths the temporally blocked kernel is instantiated for.
 constexpr int kTbMaxDepth = 8;    // 1..8: every build
@@ -83,8 +114,12 @@ void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box
 void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                unsigned* resid, hipStream_t st);
 
+// `res_level` (1..depth, 0 = depth): the fused residual (resid != null) is
+// max|level res_level - level res_level-1| -- a convergence check inside the
+// pass.
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
+             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1,
+             int res_level = 0);
 // Variant a launch of `depth` uses by default (HEAT_TB_VARIANT overrides).
 int tb_default_variant(int depth);
 // Variant tb_step picks for a launch of `depth` with this much work
@@ -100,7 +135,23 @@ bool tb_variant_deep(int variant);
 // Bit 2048: each (strip, chunk) runs on a two-wave level-split pipeline
 // (depths 8 and 12; scalar ring-3+ramp variants only).
 bool tb_variant_split(int variant);
-// Whole rounds of resident waves per launch (HEAT_TB_ROUNDS; 0 = unset: the
+// Launch-planner knobs of the TB kernel.  Defaults are the tuned values;
+// each HEAT_TB_* environment variable overrides its field when the process
+// first plans a launch (diagnostics and A/B sweeps), and tb_set_tuning()
+// replaces the whole set at run time (tests, tools).
+struct TbTuning {
+  int variant = -1;        // HEAT_TB_VARIANT: force a variant (-1: per launch)
+  int rounds = 0;          // HEAT_TB_ROUNDS: whole resident rounds per launch (0: from the work)
+  int min_len = 0;         // HEAT_TB_MINLEN: minimum chunk rows (0: max(depth, 8))
+  int waves = 0;           // HEAT_TB_WAVES: waves per launch of the solver (0: planner)
+  double edge_frac = 1.0;  // HEAT_TB_EDGE_FRAC: top/bottom edge chunk length factor
+  // HEAT_TB_AGE_WEIGHTS "w0,w1,.." (or HEAT_TB_AGE_RATIO r = {r, 1}): row
+  // shares of the age groups; empty = the built-in weights.
+  std::vector<double> age_weights;
+};
+TbTuning tb_tuning();  // a copy of the current set
+void tb_set_tuning(const TbTuning& t);
+// Whole rounds of resident waves per launch (TbTuning::rounds; 0 = unset: the
 // planner picks waves per SIMD from the work, tb_auto_waves_per_simd).
 int tb_default_rounds();
 // Resident waves of the TB kernel instantiation on the current device.
@@ -137,6 +188,25 @@ struct DeviceChecksum {
 void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, int64_t ox,
                     int64_t oy, int64_t ny, DeviceChecksum* out, hipStream_t st);
 float checksum_key_to_float(int key);
+
+// Device-side convergence decision (one per check, stream-ordered after the
+// residual of the check's pass and its all-reduce): the host never waits on a
+// check.  Unless the gate is already closed, judge_check compares the
+// residual with eps (compat mpi: double(r) <= eps, mpi/...c:245; otherwise
+// r < float(eps), cuda/cuda_heat.cu:67), closes the gate on convergence or on
+// a non-finite residual, and zeroes the residual word for the next check.
+// Every stencil launch given the gate (StencilGeom::gate = &stop) returns at
+// once after that, so passes queued behind the converging check write
+// nothing.  The host reads the record after the run.
+struct DeviceGate {
+  unsigned stop;        // gate word: non-zero once closed
+  unsigned reason;      // 1 converged, 2 non-finite residual
+  unsigned stop_check;  // ordinal (0-based, since the last reset) of the closing check
+  unsigned checks;      // checks judged while open
+  unsigned last_bits;   // residual (float bits) of the last judged check
+  unsigned pad[3];
+};
+void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st);
 
 // Max |a-b| over a box (standalone residual), atomically into *resid.
 void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,

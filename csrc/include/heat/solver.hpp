@@ -59,7 +59,9 @@ struct RunStats {
 
 class Solver {
  public:
-  Solver(const Params& p, std::unique_ptr<Transport> tr);
+  // The transport may be shared by several solvers in turn (one RCCL
+  // communicator for all the autotune candidates of a run).
+  Solver(const Params& p, std::shared_ptr<Transport> tr);
   ~Solver();
   Solver(const Solver&) = delete;
   Solver& operator=(const Solver&) = delete;
@@ -112,25 +114,57 @@ class Solver {
   float* current() { return field_[cur_]; }
 
  private:
+  // One pass of a segment: k steps, with the convergence residual taken
+  // after step rl of the pass (1..k; 0 = no check in this pass).
+  struct PassPlan {
+    int k = 0;
+    int rl = 0;
+  };
+  // What a gated run needs to restore the state of any check: the pass's
+  // first step (relative to its segment in a GraphEntry) and the host state
+  // before and after it.
+  struct PassRec {
+    int64_t step0 = 0;
+    int k = 0, rl = 0;
+    int cur0 = 0, cur1 = 0;
+    int64_t gr1 = 0, gc1 = 0;
+  };
   void alloc();
   void free_all();
   void init_fields();
   std::vector<int> pass_depths(int64_t n) const;
-  void enqueue_segment(int64_t n, bool resid);
-  void enqueue_pass(int k, bool resid);
+  // Passes for steps [step0, step0+n) with a residual level at every check
+  // point (device-gated runs: a check may fall inside a TB pass).
+  std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;
+  void enqueue_segment(const std::vector<PassPlan>& plan);
+  void enqueue_pass(int k, int rl);
   void exchange(int buf, int k, hipStream_t st);
   // `st`: the stream to launch on (nullptr = the compute stream).
-  void compute_gpu(int k, bool resid, bool split, int part, int band = 0, int64_t er = 0,
+  void compute_gpu(int k, int rl, bool split, int part, int band = 0, int64_t er = 0,
                    int64_t ec = 0, hipStream_t st = nullptr);
-  void compute_cpu(int k, bool resid, int64_t er, int64_t ec);
+  void compute_cpu(int k, int rl, int64_t er, int64_t ec);
   std::pair<int64_t, int64_t> ensure_ghosts(int k, hipStream_t st);
   float finish_resid();
   bool is_check_point(int64_t completed) const;
+  int64_t next_check_after(int64_t step) const;
   bool converged_value(float r) const;
+  // Device-gated convergence (GPU fields, device or single-rank transport):
+  // checks are judged on the device and never block the host.
+  // HEAT_HOST_CHECKS=1 forces the host-judged path (A/B diagnostics).
+  bool gated() const { return on_gpu() && P_.converge && !staged_ && !host_checks_; }
+  void run_segments(int64_t steps, RunStats& s);
+  void run_gated(int64_t steps, RunStats& s);
+  // Launch (capturing on first use) the graph or the eager enqueue of one
+  // segment; returns its pass records and check steps relative to step_.
+  void launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_t phase,
+                      bool use_graph, std::vector<PassRec>* recs, std::vector<int64_t>* checks);
+  // Re-run rl single steps from field_[cur] (the source of a pass that
+  // overshot the converging check) with the LDS kernel, ungated.
+  void replay_steps(int cur, int rl);
   void reduce_scalars(double* f64, int nf, uint64_t* u64, int nu, float* fmax, int nm);
 
   Params P_;
-  std::unique_ptr<Transport> tr_;
+  std::shared_ptr<Transport> tr_;
   Cart cart_;
   Block blk_;
   Layout L_;
@@ -138,6 +172,7 @@ class Solver {
   int T_ = 1;  // pass depth (TB depth on the GPU)
   Schedule sched_ = Schedule::Sync;
   bool staged_ = false;  // GPU fields but host-memory transport
+  bool host_checks_ = false;
   bool warmed_ = false;    // RCCL connections established outside capture
   int64_t gr_ = 0, gc_ = 0;  // ghost rows/columns of field_[cur_] at the current level
   bool comm_pending_ = false;  // comm stream has unjoined work
@@ -170,9 +205,20 @@ class Solver {
     int cur_after = 0;
     int64_t gr_after = 0, gc_after = 0;
     int64_t passes = 0, exchanges = 0;
+    std::vector<PassRec> recs;     // relative to the segment's first step
+    std::vector<int64_t> checks;   // check steps (relative), in judge order
   };
-  std::map<std::tuple<int64_t, bool, int, int64_t, int64_t>, GraphEntry> graphs_;
+  // Key: (steps, check phase or -1, cur, ghost rows, ghost cols).
+  std::map<std::tuple<int64_t, int64_t, int, int64_t, int64_t>, GraphEntry> graphs_;
   bool capturing_ = false;
+  // Gated runs: the device gate, two pinned host copies (one per segment
+  // parity) and their events; the pass log of the segment being enqueued.
+  void* d_gate_ = nullptr;
+  void* h_gate_ = nullptr;
+  hipEvent_t ev_seg_[2] = {nullptr, nullptr};
+  std::vector<PassRec> pass_log_;
+  std::vector<int64_t> check_log_;
+  bool side_interior_ = false;  // the pass's interior ran on s_comm_ (pipeline under capture)
 
   // Host-staged exchanges captured into graphs (host nodes): the arguments
   // live as long as the graphs; an error on HIP's callback thread is stored

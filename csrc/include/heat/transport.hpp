@@ -43,6 +43,16 @@ struct Msg {
   size_t rbytes = 0;
 };
 
+// What a transport reports about itself (bench JSON, tests): for RCCL the
+// communicator's own view (ncclCommCount / ncclCommCuDevice /
+// ncclCommUserRank) and the PCI bus id of its device.
+struct TransportInfo {
+  int nranks = 0;
+  int device = -1;
+  int user_rank = -1;
+  char bus_id[32] = {};
+};
+
 class Transport {
  public:
   virtual ~Transport() = default;
@@ -62,7 +72,19 @@ class Transport {
   virtual void barrier() = 0;
   // Throws if the transport has failed asynchronously (e.g. a dead peer).
   virtual void check() {}
+  // This rank gives up (e.g. a host-staged exchange failed on HIP's callback
+  // thread): make peers blocked on it fail instead of waiting.  TCP shuts its
+  // sockets down; the callback transport cannot reach into the embedding
+  // runtime, so there a peer waits for that runtime's own timeout (gloo's,
+  // bounded in bench.py by its watchdog).
+  virtual void abort() {}
   virtual const char* name() const = 0;
+  virtual TransportInfo info() const {
+    TransportInfo t;
+    t.nranks = world();
+    t.user_rank = rank();
+    return t;
+  }
 };
 
 std::unique_ptr<Transport> make_local_transport();

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void lds_kernel(const float* __restrict__ src,
                                                   float* __restrict__ dst, StencilGeom g, Box box,
                                                   int64_t c_base, unsigned* resid) {
   __shared__ float4 tile[(kLdsRows + 2) * kLdsPitch4];
+  if (tbdetail::gated(g.gate)) return;  // uniform: before the barrier
   const int64_t r0 = box.r0 + int64_t(blockIdx.y) * kLdsRows;
   const int64_t cb = c_base + int64_t(blockIdx.x) * kLdsCols;  // multiple of 4
   // Cooperative staging of rows r0-1 .. r0+kLdsRows and float4 columns

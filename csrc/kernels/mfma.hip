@@ -32,6 +32,7 @@ constexpr int kTileCols = 4;  // 16x16 tiles per wave along the columns (64 colu
 __global__ __launch_bounds__(256) void mfma_kernel(const float* __restrict__ src,
                                                    float* __restrict__ dst, StencilGeom g, Box box,
                                                    unsigned* resid) {
+  if (tbdetail::gated(g.gate)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t R = box.r0 + (int64_t(blockIdx.y) * 4 + wave) * 16;
   if (R >= box.r1) return;  // wave-uniform

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void naive_kernel(const float* __restrict__ sr
                                                     Box box, unsigned* resid) {
   const int64_t c = box.c0 + int64_t(blockIdx.x) * 64 + threadIdx.x;
   const int64_t r = box.r0 + int64_t(blockIdx.y) * 4 + threadIdx.y;
+  if (tbdetail::gated(g.gate)) return;
   unsigned m = 0;
   if (r < box.r1 && c < box.c1) {
     const int64_t i = r * g.pitch + c;
@@ -131,6 +132,27 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
     for (int64_t r = box.r0 + blockIdx.y * 4 + threadIdx.y; r < box.r1; r += gridDim.y * 4)
       m = max(m, __float_as_uint(fabsf(a[r * pitch + c] - b[r * pitch + c])));
   wave_max_atomic(m, resid);
+}
+
+__global__ void judge_kernel(unsigned* resid, DeviceGate* gate, double eps, int mpi_compat) {
+  if (threadIdx.x != 0) return;
+  if (gate->stop == 0u) {
+    const unsigned bits = *resid;
+    float r;
+    __builtin_memcpy(&r, &bits, 4);
+    const unsigned ordinal = gate->checks;
+    gate->checks = ordinal + 1u;
+    gate->last_bits = bits;
+    unsigned why = 0u;
+    if ((bits & 0x7F800000u) == 0x7F800000u) why = 2u;  // inf or NaN
+    else if (mpi_compat ? double(r) <= eps : r < float(eps)) why = 1u;
+    if (why) {
+      gate->reason = why;
+      gate->stop_check = ordinal;
+      gate->stop = 1u;
+    }
+  }
+  *resid = 0u;
 }
 
 __device__ __forceinline__ int float_key(float f) {
@@ -215,34 +237,71 @@ bool tb_depth_supported(int k) {
 int tb_strip_width(int k, int lane_cols) {
   return 64 * lane_cols - 2 * int(round_up(k, lane_cols));
 }
-int tb_lane_cols(int variant) { return (variant & 64) ? 2 : 4; }
+int tb_lane_cols(int variant) { return (variant & tbv::kFloat2) ? 2 : 4; }
 
 int tb_variant_lag(int variant) {
-  if ((variant & 3) == 3 && (variant & 8)) return 4;  // ramp + 6-row prefetch
-  switch (variant & 3) {
-    case 1: return 2;
-    case 2: return 0;
-    case 3: return 3;
+  const int pipe = variant & tbv::kPipeMask;
+  if (pipe == tbv::kRamp && (variant & tbv::kPrefetch6)) return 4;  // retired
+  switch (pipe) {
+    case tbv::kRing4: return 2;
+    case tbv::kRing2: return 0;
+    case tbv::kRamp: return 3;
     default: return 1;
   }
 }
 
 bool tb_variant_split(int variant) {
-  // Bit 2048: level-split two-wave pipelines (tb_split.hip; scalar ring-3+ramp).
-  return (variant & 2048) && (variant & 4) && !(variant & 64) && tb_variant_lag(variant) == 3;
+  // Level-split two-wave pipelines (tb_split.hip; scalar ring-3+ramp).
+  return (variant & tbv::kSplit) && tb_variant_deep(variant);
 }
 
 bool tb_variant_deep(int variant) {
-  return (variant & 4) && !(variant & 64) && tb_variant_lag(variant) == 3;
+  return (variant & tbv::kScalar) && !(variant & tbv::kFloat2) && tb_variant_lag(variant) == 3;
 }
 
-int tb_default_rounds() {
-  static const int r = [] {
-    const char* e = std::getenv("HEAT_TB_ROUNDS");
-    return e && *e ? std::max(1, std::atoi(e)) : 0;
-  }();
-  return r;
+namespace {
+TbTuning tuning_from_env() {
+  TbTuning t;
+  auto geti = [](const char* n, int def) {
+    const char* e = std::getenv(n);
+    return e && *e ? std::atoi(e) : def;
+  };
+  t.variant = geti("HEAT_TB_VARIANT", -1);
+  t.rounds = std::max(0, geti("HEAT_TB_ROUNDS", 0));
+  t.min_len = std::max(0, geti("HEAT_TB_MINLEN", 0));
+  t.waves = std::max(0, geti("HEAT_TB_WAVES", 0));
+  if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);
+  if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
+    for (const char* q = e; *q;) {
+      char* end = nullptr;
+      const double v = std::strtod(q, &end);
+      if (end == q) break;
+      t.age_weights.push_back(v);
+      q = *end == ',' ? end + 1 : end;
+    }
+  } else if (const char* r = std::getenv("HEAT_TB_AGE_RATIO"); r && *r) {
+    t.age_weights = {std::atof(r), 1.0};
+  }
+  return t;
 }
+std::mutex g_tuning_mu;
+TbTuning& tuning_ref() {
+  static TbTuning t = tuning_from_env();
+  return t;
+}
+}  // namespace
+
+TbTuning tb_tuning() {
+  std::lock_guard<std::mutex> lk(g_tuning_mu);
+  return tuning_ref();
+}
+
+void tb_set_tuning(const TbTuning& t) {
+  std::lock_guard<std::mutex> lk(g_tuning_mu);
+  tuning_ref() = t;
+}
+
+int tb_default_rounds() { return tb_tuning().rounds; }
 
 int tb_simd_count() {
   static std::map<int, int> cache;
@@ -288,42 +347,32 @@ int tb_resident_waves(int depth, int variant) {
     cache.emplace(key, w);
     return w;
   }
-  const int per_cu = (variant & 64)  ? tbn::occupancy(depth, lag)
-                     : (variant & 4) ? tbs::occupancy(depth, lag)
-                                     : tbp::occupancy(depth, lag);
+  const int per_cu = (variant & tbv::kFloat2)  ? tbn::occupancy(depth, lag)
+                     : (variant & tbv::kScalar) ? tbs::occupancy(depth, lag)
+                                                : tbp::occupancy(depth, lag);
   const int w = std::max(1, cus * std::max(1, per_cu) * 4);
   cache.emplace(key, w);
   return w;
 }
 
-namespace {
-int tb_env_variant() {
-  static const int env = [] {
-    const char* e = std::getenv("HEAT_TB_VARIANT");
-    return e && *e ? std::atoi(e) : -1;
-  }();
-  return env;
-}
-}  // namespace
-
 int tb_default_variant(int depth) {
-  if (tb_env_variant() >= 0) return tb_env_variant();
+  if (const int v = tb_tuning().variant; v >= 0) return v;
   // Ring-3 + ramp skip, scalar build, XCD-grouped blocks (23); at depth 12
   // on large launches as two-wave level-split pipelines with ds_bpermute
   // lane shifts (2071): +5 % in bench.py, +9-10 % in the interleaved kernel
   // A/B (profiles/tb_wave_timeline_r1.md).  tb_step picks per launch from
   // the work size (tb_auto_variant).
-  return depth == kTbDeepDepth ? 2071 : 23;
+  return depth == kTbDeepDepth ? tbv::kDefaultDeep : tbv::kDefault;
 }
 
 int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
-  if (tb_env_variant() >= 0) return tb_env_variant();
+  if (const int v = tb_tuning().variant; v >= 0) return v;
   // The split pipelines need about 64 strip-rows per SIMD to pay for their
   // second wave: below that (the per-rank blocks of 4-8 GPU runs: 1024 x
   // 8192, 2048 x 4096, 1536 x 8192, ...) one wave per (strip, chunk) at
   // depth 12 is 8-12 % faster, above it the split is 2-4 % faster
   // (profiles/tb_block_shapes_r2.md).
-  if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return 23;
+  if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
   return tb_default_variant(depth);
 }
 
@@ -345,19 +394,40 @@ void naive_step(const float* src, float* dst, const StencilGeom& g, const Box& b
 }
 
 namespace {
-unsigned long long* g_tb_stamps = nullptr;
-int64_t g_tb_stamp_waves = 0;
+// Stamp buffers per device: with one host thread per GPU (`heat --gpus N`)
+// each rank's launches stamp into its own device's buffer only.
+struct Stamps {
+  unsigned long long* buf = nullptr;
+  int64_t waves = 0;
+};
+std::mutex g_stamps_mu;
+std::map<int, Stamps> g_stamps;
+
+Stamps stamps_of_current_device() {
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_stamps_mu);
+  auto it = g_stamps.find(dev);
+  return it == g_stamps.end() ? Stamps{} : it->second;
+}
 }  // namespace
 
 void tb_set_stamps(unsigned long long* buf, int64_t waves) {
-  g_tb_stamps = buf;
-  g_tb_stamp_waves = waves;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_stamps_mu);
+  if (buf) g_stamps[dev] = Stamps{buf, waves};
+  else g_stamps.erase(dev);
 }
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
+             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
+             int res_level) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
+  if (res_level <= 0) res_level = depth;
+  HEAT_CHECK(res_level <= depth, "residual level %d of a depth-%d pass", res_level, depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
+  const TbTuning tune = tb_tuning();
   if (variant < 0) {
     // Both defaults use float4 lanes (same strip width).
     const int W4 = tb_strip_width(depth, 4);
@@ -380,21 +450,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   // parts) or HEAT_TB_AGE_RATIO=r (two parts r : 1) override; "1" = off.
   // Four parts (one per round at 4 blocks per CU) measured slower than two
   // whatever the weights (profiles/tb_split_age_pairs_r2.md).
-  static const std::vector<double> env_weights = [] {
-    std::vector<double> w;
-    if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
-      for (const char* q = e; *q;) {
-        char* end = nullptr;
-        const double v = std::strtod(q, &end);
-        if (end == q) break;
-        w.push_back(v);
-        q = *end == ',' ? end + 1 : end;
-      }
-    } else if (const char* r = std::getenv("HEAT_TB_AGE_RATIO"); r && *r) {
-      w = {std::atof(r), 1.0};
-    }
-    return w;
-  }();
+  const std::vector<double>& env_weights = tune.age_weights;
   const bool split_v = tb_variant_split(variant);
   int G = 0;  // age groups of this launch (0: none)
   std::vector<double> weights;
@@ -409,7 +465,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     for (double w : weights) uneven = uneven || w != weights[0] || w <= 0.0;
     G = uneven && int(weights.size()) >= 2 && int(weights.size()) <= max_groups ? int(weights.size()) : 0;
   };
-  if (variant & 256) {  // bit 256: force age groups (tests); even weights still group
+  if (variant & tbv::kForceAgePairs) {  // tests: even weights still group
     set_weights(4);
     if (G == 0) {
       G = 2;
@@ -421,7 +477,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     // SIMDs idle for the tail of the launch); by default with the number of
     // waves per SIMD chosen from the work per SIMD.
     const int resident = tb_resident_waves(depth, variant);
-    const int rounds = waves_target < 0 ? -waves_target : tb_default_rounds();
+    const int rounds = waves_target < 0 ? -waves_target : tune.rounds;
     if (rounds > 0) {
       waves_target = rounds * resident;
     } else {
@@ -432,8 +488,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       // Blocks per CU = dispatch rounds: single-wave pipelines put one wave
       // per SIMD in a block, level-split blocks hold two pipelines (4 waves).
       const int blocks_per_cu = split_v ? 2 * per_simd : per_simd;
-      // Bit 16384: never group (A/B of the weights in one process).
-      if (G == 0 && blocks_per_cu >= 2 && !(variant & 64) && !(variant & 16384))
+      if (G == 0 && blocks_per_cu >= 2 && !(variant & tbv::kFloat2) &&
+          !(variant & tbv::kNoAgePairs))
         set_weights(blocks_per_cu);
     }
   }
@@ -442,17 +498,17 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.src = src;
   args.dst = dst;
   args.resid = resid;
+  args.res_level = res_level;
   args.g = g;
-  args.flags = ((variant & 16) ? tbdetail::kTbXcdGroups : 0) |
-               ((variant & 32) ? tbdetail::kTbAltDirection : 0) |
-               ((variant & 1024) ? tbdetail::kTbDiagNoStore : 0) |
-               ((variant & 4096) ? tbdetail::kTbDiagCachedRows : 0);
+  args.flags = ((variant & tbv::kXcdGroups) ? tbdetail::kTbXcdGroups : 0) |
+               ((variant & tbv::kAltDirection) ? tbdetail::kTbAltDirection : 0) |
+               ((variant & tbv::kDiagNoStore) ? tbdetail::kTbDiagNoStore : 0) |
+               ((variant & tbv::kDiagCachedRows) ? tbdetail::kTbDiagCachedRows : 0);
   // Split rows into chunks so the whole launch has about waves_target waves,
   // but never shorter than 4*depth rows (keeps the redundant 2*depth-row
   // halo reads below ~50 %).
   // Minimum chunk length in rows (multiples of depth; HEAT_TB_MINLEN overrides).
-  const char* ml = std::getenv("HEAT_TB_MINLEN");
-  const int64_t min_len = ml && *ml ? std::max(1, std::atoi(ml)) : std::max<int64_t>(depth, 8);
+  const int64_t min_len = tune.min_len > 0 ? tune.min_len : std::max<int64_t>(depth, 8);
   int64_t len = std::max<int64_t>(min_len, ceil_div(total_strip_rows, waves_target));
   // Rows whose chunk window reaches the global top/bottom row run the
   // generic (masked) path: HEAT_TB_EDGE_FRAC < 1 gives them shorter chunks,
@@ -460,10 +516,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   // main loop: the edge chunks at 0.75 finished ~30 us before the rest of an
   // 8192^2 launch; bench.py 1.0 vs 0.95 / 0.9 / 0.75: +0.4 / +1.2 / +1.2 %
   // (profiles/tb_edge_frac_r2.md).
-  static const double edge_frac = [] {
-    const char* e = std::getenv("HEAT_TB_EDGE_FRAC");
-    return e && *e ? std::atof(e) : 1.0;
-  }();
+  const double edge_frac = tune.edge_frac;
   int n = 0, waves = 0;
   auto plan = [&](int64_t L) {
     const int64_t edge_len = std::max<int64_t>(std::min<int64_t>(min_len, L),
@@ -520,12 +573,45 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       add(bot, edge_len);
     }
   };
-  // Keep the total within waves_target (whole resident rounds): a few extra
-  // waves would form a nearly empty extra round.
-  plan(len);
-  for (int it = 0; it < 8 && waves > waves_target; ++it) {
-    len = std::max(len + 1, ceil_div(len * int64_t(waves), int64_t(waves_target)));
+  if (variant & tbv::kLinear) {
+    // Balanced plan: the boxes as one strip-row sequence cut into equal
+    // ranges, one per unit (per group of G units with age pairs), so every
+    // unit -- and every SIMD -- gets the same rows whatever the shape.  The
+    // classic (strip, chunk) plan quantises: e.g. 565 strips x 131072 rows
+    // gave 1130 two-wave pipelines for 2048 slots, 2.25 blocks per CU.
+    int64_t total = 0;
+    for (int b = 0; b < nbox; ++b) {
+      const Box& B = boxes[b];
+      if (B.empty()) continue;
+      HEAT_CHECK(B.c0 % 4 == 0, "TB box column start %lld not a multiple of 4", (long long)B.c0);
+      TbBox& t = args.box[n++];
+      t.r0 = B.r0;
+      t.r1 = B.r1;
+      t.c0 = B.c0;
+      t.c1 = B.c1;
+      t.nstrips = int(ceil_div(B.cols(), W));
+      t.nchunks = 1;
+      t.chunk_len = int(std::min<int64_t>(B.rows(), INT32_MAX));
+      t.wave_begin = 0;
+      t.lin0 = total;
+      total += int64_t(t.nstrips) * B.rows();
+    }
+    if (n == 0) return;
+    const int Gl = pairs ? G : 1;
+    const int64_t units = std::max<int64_t>(
+        Gl, std::min<int64_t>(waves_target, total / std::max<int64_t>(1, min_len)));
+    waves = int(units / Gl * Gl);
+    args.lin_total = total;
+    args.lin_slack = 2 * int64_t(depth);
+    args.flags |= tbdetail::kTbLinear;
+  } else {
+    // Keep the total within waves_target (whole resident rounds): a few extra
+    // waves would form a nearly empty extra round.
     plan(len);
+    for (int it = 0; it < 8 && waves > waves_target; ++it) {
+      len = std::max(len + 1, ceil_div(len * int64_t(waves), int64_t(waves_target)));
+      plan(len);
+    }
   }
   if (n == 0) return;
   args.nbox = n;
@@ -546,16 +632,16 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     }
   }
   const bool split = tb_variant_split(variant);
-  if (g_tb_stamps) {
+  if (const Stamps sb = stamps_of_current_device(); sb.buf) {
     const int64_t need = int64_t(waves) * (split ? 2 : 1);
-    HEAT_CHECK(need <= g_tb_stamp_waves, "stamp buffer holds %lld waves, launch has %lld",
-               (long long)g_tb_stamp_waves, (long long)need);
-    args.stamps = g_tb_stamps;
+    HEAT_CHECK(need <= sb.waves, "stamp buffer holds %lld waves, launch has %lld",
+               (long long)sb.waves, (long long)need);
+    args.stamps = sb.buf;
   }
-  const bool ok = split           ? tbx::launch_split(args, depth, st)
-                  : (variant & 64) ? tbn::launch(args, depth, lag, st)
-                  : (variant & 4)  ? tbs::launch(args, depth, lag, st)
-                                   : tbp::launch(args, depth, lag, st);
+  const bool ok = split                      ? tbx::launch_split(args, depth, st)
+                  : (variant & tbv::kFloat2) ? tbn::launch(args, depth, lag, st)
+                  : (variant & tbv::kScalar) ? tbs::launch(args, depth, lag, st)
+                                             : tbp::launch(args, depth, lag, st);
   HEAT_CHECK(ok, "TB depth %d is not instantiated for variant %d (depth %d: scalar ring-3+ramp only)",
              depth, variant, kTbDeepDepth);
   HIP_CHECK(hipGetLastError());
@@ -607,6 +693,11 @@ void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, 
   dim3 grid(unsigned(gx), unsigned(std::min<int64_t>(lx, std::max<int64_t>(1, 2048 / gx))));
   hipLaunchKernelGGL(checksum_kernel, grid, dim3(256), 0, st, origin, pitch, lx, ly, ox, oy, ny,
                      out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st) {
+  hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, gate, eps, int(mpi_compat));
   HIP_CHECK(hipGetLastError());
 }
 

@@ -13,6 +13,7 @@ namespace heat::gpu::tbdetail {
 struct TbBox {
   int64_t r0, r1, c0, c1;
   int nstrips, nchunks, chunk_len, wave_begin;
+  int64_t lin0;  // linear plans: strip-rows of the boxes before this one
 };
 
 constexpr int kMaxBoxes = 16;
@@ -36,8 +37,23 @@ struct TbArgs {
   // strip<<32 | chunk, 4 u64
   // per wave index; see tb_set_stamps().
   unsigned long long* stamps;
+  // The fused residual (resid != null) is max|level res_level - level
+  // res_level-1| over the output boxes (1..depth; a convergence check that
+  // falls inside the pass).
+  int res_level;
+  // Linear plans (kTbLinear): total strip-rows of the boxes and the slack
+  // (rows) within which a unit boundary moves to a strip end.
+  int64_t lin_total;
+  int64_t lin_slack;
   TbBox box[kMaxBoxes];
 };
+
+// Convergence gate (StencilGeom::gate): once the judge kernel has set it,
+// every later stencil launch of the run returns at once (the queued passes
+// after the converging check become no-ops).
+__device__ __forceinline__ bool gated(const unsigned* gate) {
+  return gate != nullptr && *gate != 0u;  // uniform: one scalar load per wave
+}
 
 // Launch-time layout options (variant bits 16 and 32, see tb_step):
 //   kTbXcdGroups     remap blocks so each XCD (blocks b, b+8, ... under the
@@ -63,6 +79,11 @@ constexpr int kTbDiagNoStore = 8;
 //                    chunk's first 4 rows (cache-resident; wrong results, a
 //                    probe of load latency; variant bit 4096).
 constexpr int kTbDiagCachedRows = 16;
+//   kTbLinear        balanced plan: unit u takes strip-rows [u, u+1) * total /
+//                    units of the box sequence (variant bit 32768), so every
+//                    SIMD gets the same work whatever the shape; a unit may
+//                    run several segments (strip / box / Dirichlet-mode ends).
+constexpr int kTbLinear = 32;
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
 

@@ -183,6 +183,12 @@ struct TbStream {
   vecf L0[LAG == 3 ? 6 : 1];  // LAG 3: level-0 rows t-2 .. t+3 (see lv())
   unsigned m = 0;
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
+  // RES: the residual is taken at this stage's level res_lv (1..K; 0 = not
+  // in this stage) over output rows [qb, qe) -- a convergence check inside
+  // the pass (levels < K) or at its end (K).
+  int res_lv = K;
+  int64_t qb = 0, qe = 0;
+  bool res_lane = false;  // this lane's columns are output columns of the strip
   // src / dst (run() arguments) point at the strip's first column, the same
   // for every lane (scalar registers); lane l adds lo = V * l elements, so
   // loads and stores use the scalar-base + 32-bit lane-offset addressing
@@ -197,7 +203,8 @@ struct TbStream {
   vecf* ring = nullptr;           // ring[slot * 64 + lane]
   unsigned* produced = nullptr;   // LDS, written by stage 0
   unsigned* released = nullptr;   // LDS, written by stage 1
-  int64_t seq0 = 0;               // row of sequence number 0 (the stage's first_in / rb)
+  int64_t seq0 = 0;               // row of sequence number qoff (the stage's first_in / rb)
+  int64_t qoff = 0;               // sequence number of row seq0 (segments of one unit)
   unsigned seen = 0;              // last counter value observed (polls only when needed)
 
   __device__ __forceinline__ vecf load_row(const float* __restrict__ src, int64_t row,
@@ -208,7 +215,7 @@ struct TbStream {
       // counter access (asm memory clobbers).  Acquire/release atomics would
       // also wait for this wave's in-flight global loads and stores (vmcnt)
       // and serialise the prefetch.
-      const unsigned q = unsigned(row - seq0);
+      const unsigned q = unsigned(row - seq0 + qoff);
       if (q >= seen) {
         unsigned v;
         while ((v = __hip_atomic_load(produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <= q)
@@ -237,7 +244,7 @@ struct TbStream {
                                        int64_t re, bool store_lane, int64_t* woff = nullptr) {
     if constexpr (ROLE == 1) {
       if (FAST || (ro >= rb && ro < re)) {  // every lane: stage 1 needs the overlap columns too
-        const unsigned q = unsigned(ro - seq0);
+        const unsigned q = unsigned(ro - seq0 + qoff);
         if (q >= seen + kSplitRing) {  // the slot's previous row may still be unread
           unsigned v;
           while ((v = __hip_atomic_load(released, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) +
@@ -259,9 +266,18 @@ struct TbStream {
     }
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
-      if constexpr (RES) {
-        // Columns past the box end (the last lane's spill into padding or
-        // stale ghost columns) are written but not part of the residual.
+    }
+  }
+
+  // Residual of level s, row `row` (out = the new row, b = its level s-1
+  // centre row).  s is a compile-time constant once the level loops are
+  // unrolled and res_lv / row are wave-uniform, so in the RES instantiation
+  // this costs two scalar compares per level and row; the |delta| max runs
+  // for one level only.  Columns past the box end (the last lane's spill
+  // into padding or stale ghost columns) are written but not counted.
+  __device__ __forceinline__ void res_at(int s, int64_t row, const vecf& out, const vecf& b) {
+    if constexpr (RES) {
+      if (s == res_lv && row >= qb && row < qe && res_lane) {
 #pragma unroll
         for (int j = 0; j < V; ++j)
           m = max(m, (j == 0 || rc > j) ? __float_as_uint(fabsf(out[j] - b[j])) : 0u);
@@ -289,6 +305,7 @@ struct TbStream {
         const int64_t row = i - s - 1;  // row of level s+1 computed now
         const bool ok = !ROWCHK || row_in(row, rlo, rhi);
         const vecf cn = upd(R[s][sa], R[s][sb], c, ok);
+        res_at(s + 1, row, cn, R[s][sb]);
         if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane);
         R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
         c = cn;
@@ -305,6 +322,7 @@ struct TbStream {
         R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
                                        R[s - 1][modn<RING>(U - rs)],
                                        R[s - 1][modn<RING>(U - rs + 1)], ok);
+        res_at(s, i - rs, R[s][modn<RING>(U - rs)], R[s - 1][modn<RING>(U - rs)]);
       }
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
@@ -312,6 +330,7 @@ struct TbStream {
       const vecf& b = R[K - 1][modn<RING>(U - rK)];
       const vecf out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
+      res_at(K, ro, out, b);
       emit(out, b, ro, dst, pitch, rb, re, store_lane);
     }
   }
@@ -367,12 +386,14 @@ struct TbStream {
       const bool ok = !ROWCHK || row_in(i - s, rlo, rhi);
       lv(s, T6 - s) = HEAT_TB_UPD(s, lv(s - 1, T6 - s - 1), lv(s - 1, T6 - s),
                                   lv(s - 1, T6 - s + 1), ok);
+      res_at(s, i - s, lv(s, T6 - s), lv(s - 1, T6 - s));
     }
     const int64_t ro = i - K;  // output row of this iteration
     const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
     const vecf& b = lv(K - 1, T6 - K);
     const vecf out = HEAT_TB_UPD(K, lv(K - 1, T6 - K - 1), b, lv(K - 1, T6 - K + 1), ok);
 #undef HEAT_TB_UPD
+    res_at(K, ro, out, b);
     emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
   }
 
@@ -383,6 +404,7 @@ struct TbStream {
       if constexpr (2 * S <= T) {
         const bool ok = !ROWCHK || row_in(i - S, rlo, rhi);
         lv(S, T - S) = upd(lv(S - 1, T - S - 1), lv(S - 1, T - S), lv(S - 1, T - S + 1), ok);
+        res_at(S, i - S, lv(S, T - S), lv(S - 1, T - S));
       }
       ramp_levels<T, S + 1>(i, rlo, rhi, upd);
     }
@@ -518,42 +540,24 @@ __device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, 
   return blk * per_block + sub;
 }
 
-// One work unit: a (strip, chunk) of the launch's boxes.  K1 = 0: one wave
-// runs all K levels; K1 > 0: a two-wave pipeline, stage 0 levels 1..K1
-// (into the LDS ring), stage 1 levels K1+1..K (`ring`, `cnt`: the pair's
-// LDS ring and its two counters).
+// One segment of a work unit: rows [rb, re) of one strip of box bx.  K1 =
+// 0: one wave runs all K levels; K1 > 0: a two-wave pipeline, stage 0
+// levels 1..K1 (into the LDS ring), stage 1 levels K1+1..K (`ring`, `cnt`:
+// the pair's LDS ring and its two counters; `qoff`: ring sequence number of
+// the segment's first row, so consecutive segments of one unit keep the
+// ring protocol's numbers monotonic).  Returns this lane's residual max.
 template <int K, int LAG, int K1>
-__device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
-                                       unsigned* cnt) {
+__device__ __forceinline__ unsigned tb_segment(const TbArgs& a, const TbBox& bx, int strip,
+                                               int chunk, int64_t rb, int64_t re, int stage,
+                                               vecf* ring, unsigned* cnt, int64_t qoff) {
   constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
   constexpr int W = 64 * V - 2 * KK;
   constexpr int K2 = K - K1;               // levels of stage 1
   const int lane = threadIdx.x & 63;
-  const bool pairs = a.flags & tbdetail::kTbAgePairs;
-  const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  int bi = 0;
-#pragma unroll
-  for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
-    if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
-  const TbBox bx = a.box[bi];
-  const int w = wave - bx.wave_begin;
-  const int strip = w % bx.nstrips, chunk = w / bx.nstrips;
   const int64_t cbase = bx.c0 + int64_t(strip) * W;
   const int64_t cend = min(cbase + W, bx.c1);
   const int64_t col = cbase - KK + V * lane;
   const bool store_lane = col >= cbase && col < cend;
-  int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
-  int64_t re = min(rb + bx.chunk_len, bx.r1);
-  if (pairs) {
-    // Box chunks are groups of G * chunk_len rows; age a takes rows
-    // [age_cum[a], age_cum[a+1]) / 1024 of its group.
-    const int G = a.age_groups;
-    const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
-    const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
-    rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
-    re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
-    if (rb >= re) return;
-  }
 
   const StencilGeom& g = a.g;
   const float* src = a.src + (cbase - KK);  // wave-uniform; + lo per lane
@@ -601,31 +605,51 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
     } else if constexpr (MD >= 2) {
       upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
+    // Residual level (1..K) of the launch; with two stages each takes the
+    // levels it computes (0 = none in this stage).  Output rows [rb, re)
+    // map onto themselves under the bottom-up mirror.
+    const int rl = a.res_level;
     if constexpr (K1 == 0) {
       TbStream<K, LAG, MD, decltype(res_c)::value> st;
       st.lo = V * lane;
       st.rc = int(min<int64_t>(cend - col, V));
+      st.res_lv = rl;
+      st.qb = rb;
+      st.qe = re;
+      st.res_lane = store_lane;
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     } else if (stage == 0) {
       // Level-K1 rows [rb - K2, re + K2): exactly what stage 1's trapezoid reads.
-      TbStream<K1, LAG, MD, false, 1> st;
+      TbStream<K1, LAG, MD, decltype(res_c)::value, 1> st;
       st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
       st.seq0 = rb - K2;
+      st.qoff = qoff;
+      st.rc = int(min<int64_t>(cend - col, V));
+      st.res_lv = rl <= K1 ? rl : 0;
+      st.qb = rb;
+      st.qe = re;
+      st.res_lane = store_lane;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
+      m = st.m;
     } else {
       TbStream<K2, LAG, MD, decltype(res_c)::value, 2> st;
       st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
+      st.qoff = qoff;
       st.rc = int(min<int64_t>(cend - col, V));
+      st.res_lv = rl > K1 ? rl - K1 : 0;
+      st.qb = rb;
+      st.qe = re;
+      st.res_lane = store_lane;
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
@@ -648,7 +672,101 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       break;
     default: go(std::integral_constant<int, kModeGeneric>{}); break;
   }
-  if (want_resid && (K1 == 0 || stage == 1)) wave_max_atomic(m, a.resid);
+  return m;
+}
+
+// Linear (balanced) plans: the launch's boxes are one sequence of strip-rows
+// (box-major, strip-major); unit boundaries are multiples of total/units,
+// moved to a strip end when they fall within `slack` rows of one (no tiny
+// segments, each of which would pay a whole pipeline ramp).
+__device__ __forceinline__ int64_t tb_lin_boundary(const TbArgs& a, int64_t x) {
+  if (x <= 0 || x >= a.lin_total) return min(max(x, int64_t(0)), a.lin_total);
+  int bi = 0;
+#pragma unroll
+  for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
+    if (j < a.nbox && x >= a.box[j].lin0) bi = j;
+  const int64_t rows = a.box[bi].r1 - a.box[bi].r0;
+  const int64_t r = (x - a.box[bi].lin0) % rows;
+  if (r < a.lin_slack) return x - r;
+  if (rows - r < a.lin_slack) return x + (rows - r);
+  return x;
+}
+
+// One work unit.  Classic plans: a (strip, chunk) of a box (with age pairs a
+// group of G chunks split between G units).  Linear plans: a range of the
+// strip-row sequence, run as consecutive segments (a strip end, a box end
+// or a row where the Dirichlet mode changes starts a new segment).
+template <int K, int LAG, int K1>
+__device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
+                                       unsigned* cnt) {
+  constexpr int K2 = K - K1;
+  const int lane = threadIdx.x & 63;
+  const bool pairs = a.flags & tbdetail::kTbAgePairs;
+  const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  unsigned m = 0;
+  int strip = 0, chunk = wave;
+  const bool linear = a.flags & tbdetail::kTbLinear;
+  int64_t x0 = 0, x1 = 1;  // linear: this unit's strip-row range
+  if (linear) {
+    const int64_t U = a.total_waves;
+    x0 = tb_lin_boundary(a, (a.lin_total * wave) / U);
+    x1 = tb_lin_boundary(a, (a.lin_total * (wave + 1)) / U);
+    if (pairs) {
+      const int64_t span = x1 - x0;
+      const int64_t y0 = x0 + (span * a.age_cum[age]) / 1024;
+      x1 = x0 + (span * a.age_cum[age + 1]) / 1024;
+      x0 = y0;
+    }
+  }
+  // One call site of the (large, inlined) segment body: classic plans run
+  // one segment, linear plans as many as their range crosses.
+  int64_t qoff = 0;
+  while (x0 < x1) {
+    int bi = 0;
+    int64_t rb, re;
+    if (linear) {
+#pragma unroll
+      for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
+        if (j < a.nbox && x0 >= a.box[j].lin0) bi = j;
+      const TbBox& bx = a.box[bi];
+      const int64_t rows = bx.r1 - bx.r0;
+      const int64_t off = x0 - bx.lin0;
+      strip = int(off / rows);
+      rb = bx.r0 + off % rows;
+      re = min(bx.r1, rb + (x1 - x0));
+      // Rows whose K-window reaches the plate's top / bottom row run the
+      // masked (generic) path: keep them in segments of their own.
+      const int64_t top = 1 - a.g.gx0 + K, bot = a.g.nx - 1 - a.g.gx0 - K;
+      if (rb < top && re > top) re = top;
+      else if (rb < bot && re > bot) re = bot;
+      x0 += re - rb;
+    } else {
+#pragma unroll
+      for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
+        if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
+      const TbBox& bx = a.box[bi];
+      const int w = wave - bx.wave_begin;
+      strip = w % bx.nstrips;
+      chunk = w / bx.nstrips;
+      rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
+      re = min(rb + bx.chunk_len, bx.r1);
+      if (pairs) {
+        // Box chunks are groups of G * chunk_len rows; age a takes rows
+        // [age_cum[a], age_cum[a+1]) / 1024 of its group.
+        const int G = a.age_groups;
+        const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
+        const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
+        rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
+        re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
+      }
+      x0 = x1;  // one segment
+      if (rb >= re) break;
+    }
+    m = max(m, tb_segment<K, LAG, K1>(a, a.box[bi], strip, chunk, rb, re, stage, ring, cnt, qoff));
+    qoff += (re - rb) + 2 * K2;
+  }
+  if (a.resid != nullptr && (K1 == 0 || (stage == 0) == (a.res_level <= K1)))
+    wave_max_atomic(m, a.resid);
   if (a.stamps && lane == 0) {
     const int64_t idx = int64_t(wave) + int64_t(age) * a.total_waves;
     unsigned long long* st = a.stamps + 4 * (K1 == 0 ? idx : 2 * idx + stage);
@@ -664,6 +782,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
 
 template <int K, int LAG>
 __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
+  if (tbdetail::gated(a.g.gate)) return;
   int age = 0;
   const int wave = tb_unit(a, 4, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), age);
   if (wave >= a.total_waves) return;
@@ -685,6 +804,7 @@ template <int K, int K1>
 __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_split_kernel(TbArgs a) {
   __shared__ vecf ring[2][kSplitRing * 64];
   __shared__ unsigned cnt[2][2];
+  if (tbdetail::gated(a.g.gate)) return;  // the same value for every wave of the block
   if (threadIdx.x < 4) cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
   __syncthreads();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

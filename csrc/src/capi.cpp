@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstring>
 #include <string>
@@ -97,6 +98,11 @@ struct heat_solver {
   std::unique_ptr<heat::Solver> s;
 };
 
+struct heat_transport {
+  std::shared_ptr<heat::Transport> t;
+  int device = -1;
+};
+
 namespace {
 thread_local std::string g_err;
 
@@ -114,6 +120,33 @@ int guard(F&& f) {
 }
 
 hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+std::shared_ptr<heat::Transport> make_transport(const heat_comm* c) {
+  switch (c ? c->kind : 0) {
+    case 0:
+      return heat::make_local_transport();
+    case 1:
+      return heat::make_rccl_transport(c->rank, c->world, c->unique_id, c->device);
+    case 2:
+      return heat::make_tcp_transport(c->rank, c->world, c->addr ? c->addr : "127.0.0.1", c->port);
+    case 3: {
+      heat::heat_callbacks cb{};
+      cb.ctx = c->ctx;
+      cb.rank = c->rank;
+      cb.world = c->world;
+      cb.sendrecv = reinterpret_cast<int (*)(void*, const heat::heat_msg*, int)>(c->sendrecv);
+      cb.allreduce = c->allreduce;
+      cb.barrier = c->barrier;
+      return heat::make_callback_transport(cb);
+    }
+    case 4:
+      return heat::make_loopback_transport(static_cast<heat::LoopbackHub*>(c->ctx), c->rank,
+                                           c->device);
+    default:
+      HEAT_CHECK(false, "unknown transport kind %d", c->kind);
+  }
+  return nullptr;
+}
 
 heat::gpu::StencilGeom geom(int64_t pitch, int64_t gx0, int64_t gy0, int64_t nx, int64_t ny,
                             float cx, float cy) {
@@ -168,40 +201,57 @@ int heat_loopback_hub_fail(void* hub) {
 int heat_solver_create(const heat_params* p, const heat_comm* c, heat_solver** out) {
   return guard([&] {
     heat::Params P = heat::params_from_c(p);
-    std::unique_ptr<heat::Transport> tr;
-    switch (c ? c->kind : 0) {
-      case 0:
-        tr = heat::make_local_transport();
-        break;
-      case 1:
-        tr = heat::make_rccl_transport(c->rank, c->world, c->unique_id, c->device);
-        if (P.device < 0) P.device = c->device;
-        break;
-      case 2:
-        tr = heat::make_tcp_transport(c->rank, c->world, c->addr ? c->addr : "127.0.0.1", c->port);
-        break;
-      case 3: {
-        heat::heat_callbacks cb{};
-        cb.ctx = c->ctx;
-        cb.rank = c->rank;
-        cb.world = c->world;
-        cb.sendrecv = reinterpret_cast<int (*)(void*, const heat::heat_msg*, int)>(c->sendrecv);
-        cb.allreduce = c->allreduce;
-        cb.barrier = c->barrier;
-        tr = heat::make_callback_transport(cb);
-        break;
-      }
-      case 4:
-        tr = heat::make_loopback_transport(static_cast<heat::LoopbackHub*>(c->ctx), c->rank,
-                                           c->device);
-        if (P.device < 0) P.device = c->device;
-        break;
-      default:
-        HEAT_CHECK(false, "unknown transport kind %d", c->kind);
-    }
+    std::shared_ptr<heat::Transport> tr = make_transport(c);
+    if (P.device < 0 && c && (c->kind == 1 || c->kind == 4)) P.device = c->device;
     auto* h = new heat_solver;
     try {
       h->s = std::make_unique<heat::Solver>(P, std::move(tr));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int heat_transport_create(const heat_comm* c, heat_transport** out) {
+  return guard([&] {
+    auto* t = new heat_transport;
+    try {
+      t->t = make_transport(c);
+      t->device = c && (c->kind == 1 || c->kind == 4) ? c->device : -1;
+    } catch (...) {
+      delete t;
+      throw;
+    }
+    *out = t;
+  });
+}
+
+int heat_transport_destroy(heat_transport* t) {
+  return guard([&] { delete t; });
+}
+
+int heat_transport_info_get(heat_transport* t, heat_transport_info* out) {
+  return guard([&] {
+    const heat::TransportInfo i = t->t->info();
+    std::memset(out, 0, sizeof *out);
+    out->nranks = i.nranks;
+    out->device = i.device;
+    out->user_rank = i.user_rank;
+    std::memcpy(out->bus_id, i.bus_id, sizeof out->bus_id - 1);
+    std::strncpy(out->name, t->t->name(), sizeof out->name - 1);
+  });
+}
+
+int heat_solver_create_shared(const heat_params* p, heat_transport* t, heat_solver** out) {
+  return guard([&] {
+    HEAT_CHECK(t != nullptr && t->t != nullptr, "null transport");
+    heat::Params P = heat::params_from_c(p);
+    if (P.device < 0) P.device = t->device;
+    auto* h = new heat_solver;
+    try {
+      h->s = std::make_unique<heat::Solver>(P, t->t);
     } catch (...) {
       delete h;
       throw;
@@ -393,14 +443,44 @@ int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, 
 
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes, int nbox,
-                    int depth, unsigned* resid, void* stream, int waves_target, int variant) {
+                    int depth, unsigned* resid, void* stream, int waves_target, int variant,
+                    int res_level) {
   return guard([&] {
     HEAT_CHECK(nbox >= 1 && nbox <= 5, "nbox %d", nbox);
     heat::Box b[5];
     for (int i = 0; i < nbox; ++i)
       b[i] = heat::Box{boxes[4 * i], boxes[4 * i + 1], boxes[4 * i + 2], boxes[4 * i + 3]};
     heat::gpu::tb_step(src, dst, geom(pitch, gx0, gy0, nx, ny, cx, cy), b, nbox, depth, resid,
-                       S(stream), waves_target, variant);
+                       S(stream), waves_target, variant, res_level);
+  });
+}
+
+int heat_tb_get_tuning(heat_tb_tuning* out) {
+  return guard([&] {
+    const heat::gpu::TbTuning t = heat::gpu::tb_tuning();
+    std::memset(out, 0, sizeof *out);
+    out->variant = t.variant;
+    out->rounds = t.rounds;
+    out->min_len = t.min_len;
+    out->waves = t.waves;
+    out->edge_frac = t.edge_frac;
+    out->n_weights = int32_t(std::min<size_t>(t.age_weights.size(), 4));
+    for (int i = 0; i < out->n_weights; ++i) out->weights[i] = t.age_weights[size_t(i)];
+  });
+}
+
+int heat_tb_set_tuning(const heat_tb_tuning* in) {
+  return guard([&] {
+    HEAT_CHECK(in->n_weights >= 0 && in->n_weights <= 4, "%d age weights", in->n_weights);
+    HEAT_CHECK(in->edge_frac > 0.0, "edge_frac %g", in->edge_frac);
+    heat::gpu::TbTuning t;
+    t.variant = in->variant;
+    t.rounds = std::max(0, in->rounds);
+    t.min_len = std::max(0, in->min_len);
+    t.waves = std::max(0, in->waves);
+    t.edge_frac = in->edge_frac;
+    t.age_weights.assign(in->weights, in->weights + in->n_weights);
+    heat::gpu::tb_set_tuning(t);
   });
 }
 

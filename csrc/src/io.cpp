@@ -112,12 +112,18 @@ void bin_write_block(const std::string& path, int64_t nx, int64_t ny, int64_t ox
     HEAT_CHECK(::pwrite(fd, src + r * src_pitch, size_t(n), off) == n, "row write %s",
                path.c_str());
   }
+  // Each rank makes its own rows durable before the commit barrier: ranks of
+  // a TCP run may sit on different hosts, where rank 0's fsync does not
+  // reach their page caches.
+  const int rc = ::fsync(fd);
   ::close(fd);
+  HEAT_CHECK(rc == 0, "fsync %s", path.c_str());
 }
 
 void bin_commit(const std::string& tmp, const std::string& path) {
-  // Every rank's pwrite has returned (the caller's barrier): on one node
-  // their pages are in this file's page cache, so one fsync covers them.
+  // Every rank has fsynced its rows (bin_write_block) and passed the caller's
+  // barrier: fsync the header, rename, then fsync the directory so the swap
+  // itself survives a crash (the previous checkpoint stays valid until then).
   int fd = ::open(tmp.c_str(), O_RDONLY);
   HEAT_CHECK(fd >= 0, "cannot open %s", tmp.c_str());
   const int rc = ::fsync(fd);
@@ -125,6 +131,13 @@ void bin_commit(const std::string& tmp, const std::string& path) {
   HEAT_CHECK(rc == 0, "fsync %s", tmp.c_str());
   HEAT_CHECK(::rename(tmp.c_str(), path.c_str()) == 0, "rename %s -> %s", tmp.c_str(),
              path.c_str());
+  const size_t slash = path.find_last_of('/');
+  const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+  const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  HEAT_CHECK(dfd >= 0, "cannot open directory %s", dir.c_str());
+  const int drc = ::fsync(dfd);
+  ::close(dfd);
+  HEAT_CHECK(drc == 0, "fsync directory %s", dir.c_str());
 }
 
 BinHeader bin_read_header(const std::string& path) {

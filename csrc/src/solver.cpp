@@ -37,7 +37,7 @@ void host_unpack(const float* buf, float* origin, int64_t pitch, const Box& b) {
 
 }  // namespace
 
-Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std::move(tr)) {
+Solver::Solver(const Params& p, std::shared_ptr<Transport> tr) : P_(p), tr_(std::move(tr)) {
   HEAT_CHECK(tr_ != nullptr, "no transport");
   HEAT_CHECK(P_.nx >= 1 && P_.ny >= 1, "grid %lldx%lld", (long long)P_.nx, (long long)P_.ny);
   HEAT_CHECK(P_.check_interval >= 1, "check interval %d", P_.check_interval);
@@ -98,6 +98,7 @@ Solver::Solver(const Params& p, std::unique_ptr<Transport> tr) : P_(p), tr_(std:
     sched_ = Schedule::Sync;
   L_ = Layout::make(blk_.lx, blk_.ly, H_);
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
+  host_checks_ = env_int("HEAT_HOST_CHECKS", 0) != 0;
   timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
   try {
     alloc();
@@ -137,6 +138,11 @@ void Solver::alloc() {
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
+    HIP_CHECK(hipMalloc(&d_gate_, sizeof(gpu::DeviceGate)));
+    HIP_CHECK(hipMemset(d_gate_, 0, sizeof(gpu::DeviceGate)));
+    HIP_CHECK(hipHostMalloc(&h_gate_, 2 * sizeof(gpu::DeviceGate)));
+    std::memset(h_gate_, 0, 2 * sizeof(gpu::DeviceGate));
+    for (auto& e : ev_seg_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (staged_) {
       stage_bytes_ = std::max<size_t>(size_t(H_) * size_t(L_.pitch), ew_elems) * 4;
       for (int i = 0; i < kMaxMsgs; ++i) {
@@ -185,7 +191,9 @@ void Solver::free_all() {
     if (h_resid_) (void)hipHostFree(h_resid_);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_checksum_) (void)hipFree(d_checksum_);
-    for (auto e : {ev_ready_, ev_halo_})
+    if (d_gate_) (void)hipFree(d_gate_);
+    if (h_gate_) (void)hipHostFree(h_gate_);
+    for (auto e : {ev_ready_, ev_halo_, ev_seg_[0], ev_seg_[1]})
       if (e) (void)hipEventDestroy(e);
     for (auto e : event_pool_) (void)hipEventDestroy(e);
     event_pool_.clear();
@@ -203,7 +211,8 @@ void Solver::free_all() {
   d_resid_ = nullptr;
   h_resid_ = nullptr;
   d_scratch_ = d_checksum_ = nullptr;
-  ev_ready_ = ev_halo_ = nullptr;
+  d_gate_ = h_gate_ = nullptr;
+  ev_ready_ = ev_halo_ = ev_seg_[0] = ev_seg_[1] = nullptr;
   s_comp_ = s_comm_ = nullptr;
 }
 
@@ -272,6 +281,51 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
     n -= k;
   }
   return d;
+}
+
+std::vector<Solver::PassPlan> Solver::plan_passes(int64_t step0, int64_t n) const {
+  // The pass depths of an unchecked segment, then a residual level at every
+  // check point.  A TB pass keeps its depth when one check falls inside it
+  // (the kernel takes the residual at that level; if the run converges
+  // there, replay_steps recomputes the check's state from the pass source,
+  // which no later, gated, pass overwrites).  A pass with two checks -- or a
+  // non-TB pass, whose single steps ping-pong over the source -- is cut at
+  // the first check and the rest re-split into supported depths.
+  const bool tb = tb_kernel();
+  std::vector<PassPlan> out;
+  std::deque<int> todo;
+  for (int k : pass_depths(n)) todo.push_back(k);
+  int64_t pos = step0;
+  auto push_rest = [&](int r) {
+    std::vector<int> parts;
+    while (r > 0) {
+      int d = std::min(r, T_);
+      if (tb)
+        while (!gpu::tb_depth_supported(d)) --d;
+      parts.push_back(d);
+      r -= d;
+    }
+    for (auto it = parts.rbegin(); it != parts.rend(); ++it) todo.push_front(*it);
+  };
+  while (!todo.empty()) {
+    const int k = todo.front();
+    todo.pop_front();
+    const int64_t c = P_.converge ? next_check_after(pos) : INT64_MAX;
+    if (c > pos + k) {
+      out.push_back({k, 0});
+    } else {
+      const int k1 = int(c - pos);
+      const bool second = next_check_after(c) <= pos + k;
+      if (k1 == k || (tb && !second)) {
+        out.push_back({k, k1});
+      } else {
+        out.push_back({k1, k1});
+        push_rest(k - k1);
+      }
+    }
+    pos += out.back().k;
+  }
+  return out;
 }
 
 // ---------------------------------------------------------------------------
@@ -381,9 +435,14 @@ void Solver::staged_host_fn(void* p) {
   try {
     self->tr_->sendrecv(c->msgs.data(), int(c->msgs.size()), nullptr);
   } catch (const std::exception& e) {
-    std::lock_guard<std::mutex> lk(self->staged_mu_);
-    self->staged_error_ = e.what();
-    self->staged_failed_.store(true);
+    {
+      std::lock_guard<std::mutex> lk(self->staged_mu_);
+      self->staged_error_ = e.what();
+      self->staged_failed_.store(true);
+    }
+    // Later staged nodes of this rank are skipped, so its peers would wait
+    // for messages that never come: let the transport fail them now.
+    self->tr_->abort();
   }
 }
 
@@ -396,7 +455,7 @@ void Solver::check_staged() {
 // ---------------------------------------------------------------------------
 // compute
 // ---------------------------------------------------------------------------
-void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int64_t er,
+void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t er,
                          int64_t ec, hipStream_t st) {
   if (!st) st = s_comp_;
   // Host-side enqueue range (interior / boundary bands of the overlap
@@ -415,10 +474,11 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
   g.cx = P_.cx;
   g.cy = P_.cy;
   g.numerics = int(P_.numerics);
-  unsigned* r = resid ? d_resid_ : nullptr;
+  if (gated()) g.gate = static_cast<const unsigned*>(d_gate_);  // DeviceGate::stop
+  unsigned* r = rl > 0 ? d_resid_ : nullptr;
   const int64_t lx = blk_.lx, ly = blk_.ly;
   const auto& nb = blk_.nbr;
-  static const int waves_target = env_int("HEAT_TB_WAVES", 0);
+  const int waves_target = gpu::tb_tuning().waves;
   // The box of this pass: the owned block grown by (er, ec) into the ghost
   // ring on sides that have a neighbour (deep-halo passes).
   const Box own{nb[North] >= 0 ? -er : 0, lx + (nb[South] >= 0 ? er : 0),
@@ -432,19 +492,20 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
             nb[West] >= 0 ? own.c0 - e : 0, own.c1 + (nb[East] >= 0 ? e : 0)};
       const float* a = field_[cur_];
       float* d = field_[cur_ ^ 1];
+      unsigned* rj = j == rl - 1 ? r : nullptr;
       if (P_.kernel == KernelKind::Lds)
-        gpu::lds_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
+        gpu::lds_step(a, d, g, b, rj, st);
       else if (P_.kernel == KernelKind::Mfma)
-        gpu::mfma_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
+        gpu::mfma_step(a, d, g, b, rj, st);
       else
-        gpu::naive_step(a, d, g, b, j == k - 1 ? r : nullptr, st);
+        gpu::naive_step(a, d, g, b, rj, st);
       cur_ ^= 1;
     }
     return;
   }
 
   if (!split) {
-    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target, -1, rl);
     return;
   }
   // Boundary bands are `band` >= k deep (k for exchange-first; H for the
@@ -456,15 +517,15 @@ void Solver::compute_gpu(int k, bool resid, bool split, int part, int band, int6
   const int64_t c1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
   if (part == 0) {
     Box in{r0, r1, c0, c1};
-    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target, -1, rl);
   } else {
     Box b[4] = {{0, r0, 0, ly}, {r1, lx, 0, ly}, {r0, r1, 0, c0}, {r0, r1, c1, ly}};
-    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target, -1, rl);
     // cur_ flips once per pass, after the boundary part.
   }
 }
 
-void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
+void Solver::compute_cpu(int k, int rl, int64_t er, int64_t ec) {
   TraceRange trace("heat.compute");
   PhaseScope phase(this, kCompute, nullptr);
   cpu::Geom g;
@@ -481,16 +542,22 @@ void Solver::compute_cpu(int k, bool resid, int64_t er, int64_t ec) {
     const int64_t e = k - 1 - j;
     Box b{nb[North] >= 0 ? -(er + e) : 0, blk_.lx + (nb[South] >= 0 ? er + e : 0),
           nb[West] >= 0 ? -(ec + e) : 0, blk_.ly + (nb[East] >= 0 ? ec + e : 0)};
-    const bool last = j == k - 1;
-    float r = cpu::step(field_[cur_], field_[cur_ ^ 1], g, b, resid && last);
-    if (resid && last) cpu_resid_ = r;
+    const bool at = j == rl - 1;
+    float r = cpu::step(field_[cur_], field_[cur_ ^ 1], g, b, at);
+    if (at) cpu_resid_ = r;
     cur_ ^= 1;
   }
 }
 
 std::pair<int64_t, int64_t> Solver::ensure_ghosts(int k, hipStream_t st) {
   // gr_/gc_: how many ghost rows/columns of field_[cur_] hold the current
-  // time level.  A k-step pass needs k; an exchange refills H.  The pass
+  // time level.  A k-step pass needs k; an exchange refills H.  Invariant:
+  // they never exceed the depth of the last exchange of this buffer -- N/S
+  // row messages carry the sender's own (stale) ghost columns into our
+  // corners, and only the corner unpack of THAT exchange overwrites them up
+  // to its depth (the overlap schedule exchanges k < H and then claims 0;
+  // tests/test_gpu_loopback.py::test_loopback_deep_halo_chunked mixes depths
+  // and short tail segments on 2 x 2 ranks).  The pass
   // then also updates the (valid - k) ghost rows/columns next to the block,
   // which become the valid ghosts of the next level.  Only axes that are
   // decomposed count, so every rank makes the same decision.
@@ -499,6 +566,8 @@ std::pair<int64_t, int64_t> Solver::ensure_ghosts(int k, hipStream_t st) {
     exchange(cur_, H_, st);
     gr_ = gc_ = H_;
   }
+  HEAT_CHECK(gr_ <= H_ && gc_ <= H_, "ghost depth %lld/%lld beyond the exchanged %d",
+             (long long)gr_, (long long)gc_, H_);
   // TB boxes start on a float4 column: round the column extension down.
   const bool tb = tb_kernel();
   const int64_t er = ns ? gr_ - k : 0;
@@ -508,12 +577,19 @@ std::pair<int64_t, int64_t> Solver::ensure_ghosts(int k, hipStream_t st) {
   return {er, ec};
 }
 
-void Solver::enqueue_pass(int k, bool resid) {
+void Solver::enqueue_pass(int k, int rl) {
   const auto& nb = blk_.nbr;
+  const bool resid = rl > 0;
   // With world > 1 every rank of the (non-periodic) grid has a neighbour.
   const bool multi = tr_->world() > 1;
+  PassRec rec;
+  rec.step0 = step_;
+  rec.k = k;
+  rec.rl = rl;
+  rec.cur0 = cur_;
   if (on_gpu()) {
-    if (resid) HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
+    // Gated runs zero the residual word in the judge kernel instead.
+    if (resid && !gated()) HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
     const bool tb = tb_kernel();
     const int64_t lx = blk_.lx, ly = blk_.ly;
     const int band = sched_ == Schedule::Pipeline ? H_ : k;
@@ -530,8 +606,9 @@ void Solver::enqueue_pass(int k, bool resid) {
     // tools/rccl_mr_diag.sh), and a graph has the same dependency DAG either
     // way (exchange || interior, then the bands).
     const bool comm_on_side = !(capturing_ && tr_->device_memory());
+    side_interior_ = false;
     if (!multi) {
-      compute_gpu(k, resid, false, 0);
+      compute_gpu(k, rl, false, 0);
     } else if (sched_ == Schedule::Pipeline) {
       // Boundary-first: the H-deep ghosts of cur_ were exchanged by the
       // previous pass (or now, if stale).  Compute the H-deep boundary bands,
@@ -552,19 +629,20 @@ void Solver::enqueue_pass(int k, bool resid) {
       // joining the comm stream, and a captured graph may not wait on an
       // event recorded outside its capture.
       if (comm_pending_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-      compute_gpu(k, resid, true, 1, band);
+      compute_gpu(k, rl, true, 1, band);
       HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
       if (comm_on_side) {
         // The interior is enqueued before the exchange: the stream semantics
         // are the same (s_comm waits for the bands only), and a host-staged
         // exchange, which blocks the host, then overlaps the interior too.
-        compute_gpu(k, resid, true, 0, band);
+        compute_gpu(k, rl, true, 0, band);
         HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
         exchange(cur_ ^ 1, H_, s_comm_);
       } else {
         HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-        compute_gpu(k, resid, true, 0, band, 0, 0, s_comm_);
+        compute_gpu(k, rl, true, 0, band, 0, 0, s_comm_);
         exchange(cur_ ^ 1, H_, s_comp_);
+        side_interior_ = true;
       }
       HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
       comm_pending_ = true;
@@ -576,43 +654,57 @@ void Solver::enqueue_pass(int k, bool resid) {
       if (comm_on_side) {
         exchange(cur_, k, s_comm_);
         HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-        compute_gpu(k, resid, true, 0);
+        compute_gpu(k, rl, true, 0);
       } else {
-        compute_gpu(k, resid, true, 0, 0, 0, 0, s_comm_);
+        compute_gpu(k, rl, true, 0, 0, 0, 0, s_comm_);
         HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
         exchange(cur_, k, s_comp_);
       }
       HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-      compute_gpu(k, resid, true, 1);
+      compute_gpu(k, rl, true, 1);
       gr_ = gc_ = 0;
     } else if (sched_ == Schedule::Overlap) {
       exchange(cur_, k, s_comp_);
-      compute_gpu(k, resid, false, 0);
+      compute_gpu(k, rl, false, 0);
       gr_ = gc_ = 0;
     } else {
       // Sync (default): one launch per pass, one exchange per H/k passes.
       const auto ext = ensure_ghosts(k, s_comp_);
-      compute_gpu(k, resid, false, 0, 0, ext.first, ext.second);
+      compute_gpu(k, rl, false, 0, 0, ext.first, ext.second);
     }
     if (tb) cur_ ^= 1;
     if (resid) {
       TraceRange trace("heat.allreduce");
       PhaseScope phase(this, kReduce, s_comp_);
-      if (tr_->device_memory()) tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
-      HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
+      // The residual is complete only once every launch of the pass is:
+      // join the interior the pipeline ran on the comm stream (ev_halo_ was
+      // recorded right behind it) before the all-reduce reads the word.
+      if (side_interior_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+      const bool dev = tr_->device_memory();
+      if (dev && multi) tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
+      if (gated()) {
+        gpu::judge_check(d_resid_, static_cast<gpu::DeviceGate*>(d_gate_), P_.eps,
+                         P_.compat == Compat::Mpi, s_comp_);
+        check_log_.push_back(step_ + rl);
+      } else {
+        HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, 4, hipMemcpyDeviceToHost, s_comp_));
+      }
     }
   } else {
     std::pair<int64_t, int64_t> ext{0, 0};
     if (multi) ext = ensure_ghosts(k, nullptr);
-    compute_cpu(k, resid, ext.first, ext.second);
+    compute_cpu(k, rl, ext.first, ext.second);
   }
+  rec.cur1 = cur_;
+  rec.gr1 = gr_;
+  rec.gc1 = gc_;
+  pass_log_.push_back(rec);
   step_ += k;
   ++stat_passes_;
 }
 
-void Solver::enqueue_segment(int64_t n, bool resid) {
-  auto d = pass_depths(n);
-  for (size_t i = 0; i < d.size(); ++i) enqueue_pass(d[i], resid && i + 1 == d.size());
+void Solver::enqueue_segment(const std::vector<PassPlan>& plan) {
+  for (const PassPlan& p : plan) enqueue_pass(p.k, p.rl);
   if (comm_pending_) {
     // Join the comm stream (the last pass posted the next exchange): a
     // captured graph must end on its origin stream, and the next segment
@@ -695,6 +787,14 @@ bool Solver::is_check_point(int64_t completed) const {
   return completed >= 1 && completed % C == 0;
 }
 
+int64_t Solver::next_check_after(int64_t step) const {
+  // Canonical: after steps C, 2C, ...; compat cuda: after steps 1, C+1, 2C+1
+  // (cuda/cuda_heat.cu:219 checks at i % 20 == 0, 0-based).
+  const int64_t C = P_.check_interval;
+  if (P_.compat == Compat::Cuda) return step < 1 ? 1 : ((step - 1) / C + 1) * C + 1;
+  return (step / C + 1) * C;
+}
+
 bool Solver::converged_value(float r) const {
   // mpi/...c:245 compares the fp32 |delta| against the double 1e-3;
   // cuda/cuda_heat.cu:67 compares in fp32 against 1e-3f.
@@ -702,90 +802,123 @@ bool Solver::converged_value(float r) const {
   return r < float(P_.eps);
 }
 
-RunStats Solver::run(int64_t steps) {
-  TraceRange trace("heat.run");
-  RunStats s;
-  HEAT_CHECK(steps >= 0, "negative step count");
-  const int64_t p0 = stat_passes_, e0 = stat_exchanges_;
-  synchronize();
-  const double t0 = now_s();
+void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_t phase,
+                            bool use_graph, std::vector<PassRec>* recs,
+                            std::vector<int64_t>* checks) {
+  // Records come back relative to the segment's first step.
+  const int64_t step_before = step_;
+  auto relative = [&](GraphEntry& e) {
+    e.recs = std::move(pass_log_);
+    e.checks = std::move(check_log_);
+    for (auto& r : e.recs) r.step0 -= step_before;
+    for (auto& c : e.checks) c -= step_before;
+    pass_log_.clear();
+    check_log_.clear();
+  };
+  pass_log_.clear();
+  check_log_.clear();
+  if (!use_graph) {
+    enqueue_segment(plan);
+    GraphEntry e;
+    relative(e);
+    *recs = std::move(e.recs);
+    *checks = std::move(e.checks);
+    return;
+  }
+  const auto key = std::make_tuple(n, phase, cur_, gr_, gc_);
+  auto it = graphs_.find(key);
+  if (it == graphs_.end()) {
+    const int64_t p_before = stat_passes_, e_before = stat_exchanges_;
+    TraceRange trace_capture("heat.capture");
+    hipGraph_t graph;
+    HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
+    capturing_ = true;
+    try {
+      enqueue_segment(plan);
+    } catch (...) {
+      capturing_ = false;
+      hipGraph_t g2;
+      (void)hipStreamEndCapture(s_comp_, &g2);
+      throw;
+    }
+    capturing_ = false;
+    HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
+    GraphEntry e;
+    HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(graph));
+    e.cur_after = cur_;
+    e.gr_after = gr_;
+    e.gc_after = gc_;
+    e.passes = stat_passes_ - p_before;
+    e.exchanges = stat_exchanges_ - e_before;
+    relative(e);
+    stat_passes_ = p_before;
+    stat_exchanges_ = e_before;
+    it = graphs_.emplace(key, std::move(e)).first;
+  }
+  HIP_CHECK(hipGraphLaunch(it->second.exec, s_comp_));
+  cur_ = it->second.cur_after;
+  gr_ = it->second.gr_after;
+  gc_ = it->second.gc_after;
+  step_ = step_before + n;
+  stat_passes_ += it->second.passes;
+  stat_exchanges_ += it->second.exchanges;
+  *recs = it->second.recs;
+  *checks = it->second.checks;
+}
+
+void Solver::replay_steps(int cur, int rl) {
+  // rl single LDS-kernel steps from field_[cur], ungated, over the owned
+  // block grown by the steps still to come on sides with a neighbour (the
+  // source's ghosts are valid that deep: the overshooting pass read k > rl
+  // of them).  Bitwise the same arithmetic as the TB kernel.
+  TraceRange trace("heat.replay");
+  gpu::StencilGeom g;
+  g.pitch = L_.pitch;
+  g.gx0 = blk_.ox;
+  g.gy0 = blk_.oy;
+  g.nx = P_.nx;
+  g.ny = P_.ny;
+  g.cx = P_.cx;
+  g.cy = P_.cy;
+  g.numerics = int(P_.numerics);
+  const auto& nb = blk_.nbr;
+  for (int j = 0; j < rl; ++j) {
+    const int64_t e = rl - 1 - j;
+    const Box b{nb[North] >= 0 ? -e : 0, blk_.lx + (nb[South] >= 0 ? e : 0),
+                nb[West] >= 0 ? -e : 0, blk_.ly + (nb[East] >= 0 ? e : 0)};
+    gpu::lds_step(field_[cur], field_[cur ^ 1], g, b, nullptr, s_comp_);
+    cur ^= 1;
+  }
+  cur_ = cur;
+  gr_ = gc_ = 0;
+}
+
+void Solver::run_segments(int64_t steps, RunStats& s) {
+  // Host-judged path (CPU backend, host-staged transports): one segment per
+  // check, a host round trip per check.
   const bool gpu = on_gpu();
-  // Staged (host-memory) transports are captured as host nodes.
   const bool can_graph = gpu && P_.use_graph && !timing_ &&
                          (tr_->world() == 1 || tr_->graph_capturable() || staged_) &&
                          env_int("HEAT_GRAPH", 1) != 0;
-  if (timing_) {
-    spans_.clear();
-    pool_used_ = 0;
-    phase_acc_[0] = phase_acc_[1] = phase_acc_[2] = 0.0;
-  }
-  if (can_graph && tr_->world() > 1 && tr_->device_memory() && !warmed_) {
-    // Let RCCL establish its connections outside of stream capture.  A halo
-    // exchange of the current buffer is idempotent.
-    exchange(cur_, H_, s_comp_);
-    tr_->allreduce_max(reinterpret_cast<float*>(d_scratch_), 1, s_comp_);
-    HIP_CHECK(hipStreamSynchronize(s_comp_));
-    warmed_ = true;
-  }
   int64_t remaining = steps;
+  std::vector<PassRec> recs;
+  std::vector<int64_t> checks;
   while (remaining > 0) {
     int64_t seg = remaining;
     bool resid = false;
     if (P_.converge) {
-      int64_t next;
-      if (P_.compat == Compat::Cuda)
-        next = step_ < 1 ? 1 : ((step_ - 1) / P_.check_interval + 1) * P_.check_interval + 1;
-      else
-        next = (step_ / P_.check_interval + 1) * P_.check_interval;
+      const int64_t next = next_check_after(step_);
       if (next - step_ <= remaining) {
         seg = next - step_;
         resid = true;
       }
     }
-    if (can_graph) {
-      const auto key = std::make_tuple(seg, resid, cur_, gr_, gc_);
-      auto it = graphs_.find(key);
-      const int cur_before = cur_;
-      const int64_t step_before = step_;
-      if (it == graphs_.end()) {
-        const int64_t p_before = stat_passes_, e_before = stat_exchanges_;
-        TraceRange trace_capture("heat.capture");
-        hipGraph_t graph;
-        HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
-        capturing_ = true;
-        try {
-          enqueue_segment(seg, resid);
-        } catch (...) {
-          capturing_ = false;
-          hipGraph_t g2;
-          (void)hipStreamEndCapture(s_comp_, &g2);
-          throw;
-        }
-        capturing_ = false;
-        HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
-        GraphEntry e;
-        HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
-        HIP_CHECK(hipGraphDestroy(graph));
-        e.cur_after = cur_;
-        e.gr_after = gr_;
-        e.gc_after = gc_;
-        e.passes = stat_passes_ - p_before;
-        e.exchanges = stat_exchanges_ - e_before;
-        stat_passes_ = p_before;
-        stat_exchanges_ = e_before;
-        it = graphs_.emplace(key, e).first;
-      }
-      HIP_CHECK(hipGraphLaunch(it->second.exec, s_comp_));
-      cur_ = it->second.cur_after;
-      gr_ = it->second.gr_after;
-      gc_ = it->second.gc_after;
-      step_ = step_before + seg;
-      stat_passes_ += it->second.passes;
-      stat_exchanges_ += it->second.exchanges;
-      (void)cur_before;
-    } else {
-      enqueue_segment(seg, resid);
-    }
+    const auto d = pass_depths(seg);
+    std::vector<PassPlan> plan;
+    for (size_t i = 0; i < d.size(); ++i)
+      plan.push_back({d[i], resid && i + 1 == d.size() ? d[i] : 0});
+    launch_segment(plan, seg, resid ? 0 : -1, can_graph, &recs, &checks);
     remaining -= seg;
     s.steps_done += seg;
     if (resid) {
@@ -801,6 +934,112 @@ RunStats Solver::run(int64_t steps) {
         break;
       }
     }
+  }
+}
+
+void Solver::run_gated(int64_t steps, RunStats& s) {
+  // Device-judged path: segments of whole check periods are enqueued without
+  // waiting on any check (two in flight; the host polls a pinned copy of the
+  // gate one segment behind).  Checks inside a pass are taken at their
+  // level; after the converging check every stencil launch is a no-op, so
+  // the state of that check is either a pass output or, for a check inside
+  // a pass, recomputed from the pass source (replay_steps).
+  const bool can_graph = P_.use_graph && !timing_ &&
+                         (tr_->world() == 1 || tr_->graph_capturable()) &&
+                         env_int("HEAT_GRAPH", 1) != 0;
+  const int64_t C = P_.check_interval;
+  // ~512 steps per segment, a whole number of check periods: every segment
+  // of a run starts at the same check phase (one graph per shape).
+  const int64_t seg_cap = C * std::max<int64_t>(1, (512 + C - 1) / C);
+  auto* gate_h = static_cast<gpu::DeviceGate*>(h_gate_);
+  HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(gpu::DeviceGate), s_comp_));
+  HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
+  const int64_t step0 = step_;
+  std::vector<PassRec> all_recs;
+  std::vector<int64_t> all_checks;
+  int64_t remaining = steps, j = 0;
+  bool stopped = false;
+  while (remaining > 0 && !stopped) {
+    const int64_t seg = std::min(remaining, seg_cap);
+    const int64_t base = step_;
+    const int64_t phase = next_check_after(step_) - step_;
+    std::vector<PassRec> recs;
+    std::vector<int64_t> checks;
+    launch_segment(plan_passes(step_, seg), seg, phase, can_graph, &recs, &checks);
+    for (auto& r : recs) {
+      r.step0 += base;
+      all_recs.push_back(r);
+    }
+    for (auto c : checks) all_checks.push_back(c + base);
+    HIP_CHECK(hipMemcpyAsync(&gate_h[j & 1], d_gate_, sizeof(gpu::DeviceGate),
+                             hipMemcpyDeviceToHost, s_comp_));
+    HIP_CHECK(hipEventRecord(ev_seg_[j & 1], s_comp_));
+    if (j >= 1) {
+      HIP_CHECK(hipEventSynchronize(ev_seg_[(j - 1) & 1]));
+      stopped = gate_h[(j - 1) & 1].stop != 0;
+    }
+    remaining -= seg;
+    ++j;
+  }
+  synchronize();
+  const gpu::DeviceGate gate = gate_h[(j - 1) & 1];
+  s.checks = gate.checks;
+  if (gate.checks > 0) std::memcpy(&s.last_resid, &gate.last_bits, 4);
+  if (!gate.stop) {
+    s.steps_done = step_ - step0;
+    return;
+  }
+  HEAT_CHECK(gate.stop_check < all_checks.size(), "gate closed at check %u of %zu",
+             gate.stop_check, all_checks.size());
+  const int64_t c = all_checks[gate.stop_check];
+  if (gate.reason == 2)
+    throw_error(__FILE__, __LINE__,
+                strprintf("non-finite residual (%g) at step %lld", double(s.last_resid),
+                          (long long)c));
+  const PassRec* p = nullptr;
+  for (const auto& r : all_recs)
+    if (r.step0 < c && c <= r.step0 + r.k) p = &r;
+  HEAT_CHECK(p != nullptr && p->rl == c - p->step0, "no pass holds check step %lld",
+             (long long)c);
+  if (p->rl == p->k) {
+    cur_ = p->cur1;
+    gr_ = p->gr1;
+    gc_ = p->gc1;
+  } else {
+    replay_steps(p->cur0, p->rl);
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+  }
+  step_ = c;
+  s.steps_done = c - step0;
+  s.converged = true;
+  s.converged_at = c;
+}
+
+RunStats Solver::run(int64_t steps) {
+  TraceRange trace("heat.run");
+  RunStats s;
+  HEAT_CHECK(steps >= 0, "negative step count");
+  const int64_t p0 = stat_passes_, e0 = stat_exchanges_;
+  synchronize();
+  const double t0 = now_s();
+  const bool gpu = on_gpu();
+  if (timing_) {
+    spans_.clear();
+    pool_used_ = 0;
+    phase_acc_[0] = phase_acc_[1] = phase_acc_[2] = 0.0;
+  }
+  const bool graphs = gpu && P_.use_graph && !timing_ && env_int("HEAT_GRAPH", 1) != 0;
+  if (graphs && tr_->world() > 1 && tr_->device_memory() && tr_->graph_capturable() && !warmed_) {
+    // Let RCCL establish its connections outside of stream capture.  A halo
+    // exchange of the current buffer is idempotent.
+    exchange(cur_, H_, s_comp_);
+    tr_->allreduce_max(reinterpret_cast<float*>(d_scratch_), 1, s_comp_);
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    warmed_ = true;
+  }
+  if (steps > 0) {
+    if (gated()) run_gated(steps, s);
+    else run_segments(steps, s);
   }
   synchronize();
   check_staged();

@@ -82,6 +82,15 @@ class RcclTransport final : public Transport {
                   std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
   }
   const char* name() const override { return "rccl"; }
+  TransportInfo info() const override {
+    TransportInfo t;
+    NCCL_CHECK(ncclCommCount(comm_, &t.nranks));
+    NCCL_CHECK(ncclCommCuDevice(comm_, &t.device));
+    NCCL_CHECK(ncclCommUserRank(comm_, &t.user_rank));
+    if (hipDeviceGetPCIBusId(t.bus_id, int(sizeof t.bus_id), t.device) != hipSuccess)
+      t.bus_id[0] = 0;
+    return t;
+  }
 
  private:
   int rank_, world_;

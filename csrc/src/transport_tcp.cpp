@@ -174,6 +174,10 @@ class TcpTransport final : public Transport {
         ::fcntl(fds_[size_t(i)], F_SETFL, ::fcntl(fds_[size_t(i)], F_GETFL) | O_NONBLOCK);
       }
   }
+  void abort() override {
+    for (int fd : fds_)
+      if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // peers' reads on these sockets fail at once
+  }
   ~TcpTransport() override {
     for (int fd : fds_)
       if (fd >= 0) ::close(fd);

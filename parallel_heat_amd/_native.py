@@ -22,7 +22,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be imported before libheat: shared HIP runtime)
 
-ABI_VERSION = 2  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
+ABI_VERSION = 3  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
@@ -98,6 +98,17 @@ class HeatBlockInfo(Structure):
     ]
 
 
+class HeatTransportInfo(Structure):
+    _fields_ = [("nranks", c_int32), ("device", c_int32), ("user_rank", c_int32),
+                ("bus_id", ctypes.c_char * 32), ("name", ctypes.c_char * 16)]
+
+
+class HeatTbTuning(Structure):
+    _fields_ = [("variant", c_int32), ("rounds", c_int32), ("min_len", c_int32),
+                ("waves", c_int32), ("edge_frac", c_double), ("n_weights", c_int32),
+                ("pad_", c_int32), ("weights", c_double * 4)]
+
+
 class HeatChecksum(Structure):
     _fields_ = [("hash", c_uint64), ("sum", c_double), ("min", c_double), ("max", c_double),
                 ("count", c_int64)]
@@ -111,6 +122,10 @@ _SIGS = {
     "heat_device_count": (c_int, [POINTER(c_int)]),
     "heat_solver_create": (c_int, [POINTER(HeatParams), POINTER(HeatComm), POINTER(c_void_p)]),
     "heat_solver_destroy": (c_int, [c_void_p]),
+    "heat_transport_create": (c_int, [POINTER(HeatComm), POINTER(c_void_p)]),
+    "heat_transport_destroy": (c_int, [c_void_p]),
+    "heat_transport_info_get": (c_int, [c_void_p, POINTER(HeatTransportInfo)]),
+    "heat_solver_create_shared": (c_int, [POINTER(HeatParams), c_void_p, POINTER(c_void_p)]),
     "heat_solver_run": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
     "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
     "heat_rccl_self_test": (c_int, [c_int, c_int64, c_int, c_int, POINTER(c_double)]),
@@ -148,7 +163,9 @@ _SIGS = {
                                   c_void_p, c_void_p]),
     "heat_op_tb_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                 c_float, c_float, POINTER(c_int64), c_int, c_int, c_void_p,
-                                c_void_p, c_int, c_int]),
+                                c_void_p, c_int, c_int, c_int]),
+    "heat_tb_get_tuning": (c_int, [POINTER(HeatTbTuning)]),
+    "heat_tb_set_tuning": (c_int, [POINTER(HeatTbTuning)]),
     "heat_op_tb_stamps": (c_int, [c_void_p, c_int64]),
     "heat_op_init": (c_int, [c_void_p, c_int64, c_int64, c_int, c_int64, c_int64, c_int64,
                              c_int64, c_int, c_uint64, c_void_p]),
@@ -246,7 +263,7 @@ def rccl_unique_id() -> bytes:
 
 
 __all__ = [
-    "HeatParams", "HeatComm", "HeatMsg", "HeatRunStats", "HeatBlockInfo", "HeatChecksum",
+    "HeatParams", "HeatComm", "HeatMsg", "HeatTransportInfo", "HeatTbTuning", "HeatRunStats", "HeatBlockInfo", "HeatChecksum",
     "SENDRECV_CB", "ALLREDUCE_CB", "BARRIER_CB", "NativeError", "lib", "call", "check",
     "available", "build_native", "loaded_path", "device_count", "rccl_unique_id",
     "require_gpu_native", "LIB_PATH", "CLI_PATH", "c_uint",

@@ -1,15 +1,20 @@
 """``python -m parallel_heat_amd`` — the Python front end of the ``heat`` CLI.
 
-Same flags as the native ``build/heat`` binary.  Multi-rank runs are launched
-with ``python -m torch.distributed.run --nproc-per-node N -m parallel_heat_amd
-...``: GPU ranks talk over the engine's RCCL communicator, CPU ranks over
-torch.distributed (gloo).  Replaces the reference's -D macro builds
+Same flags as the native ``build/heat`` binary (tests/test_cli.py pins the
+two flag sets and their reference output lines against each other).
+Multi-rank runs are launched with ``python -m torch.distributed.run
+--nproc-per-node N -m parallel_heat_amd ...``: GPU ranks talk over the
+engine's RCCL communicator, CPU ranks over torch.distributed (gloo).  The
+single-process native modes -- ``--gpus N`` (N GPU ranks as threads of one
+process) and ``--plan`` (the per-GPU memory plan) -- run the native binary
+with the same arguments.  ``--transport torch`` is the one Python-only value.  Replaces the reference's -D macro builds
 (``cuda/Makefile``, ``mpi/Makefile:12-22``) with run-time flags.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import subprocess
 import sys
 
 import torch
@@ -55,6 +60,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--numerics", choices=["fp32", "mpi"], default="fp32")
     a("--phase-timing", action="store_true")
     a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
+    a("--port", type=int, default=0, help="tcp transport rendezvous port (0: MASTER_PORT+1)")
+    a("--gpus", type=int, default=0, help="one process, N GPU ranks as threads (native binary)")
+    a("--plan", action="store_true", help="print the per-GPU memory plan and exit (native)")
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
     a("--resume", default=None)
@@ -63,7 +71,12 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
+    if args.gpus > 0 or args.plan:
+        # Single-process native modes: the `heat` binary owns the threads
+        # and the planner; same flags, same output.
+        return subprocess.run([str(_native.CLI_PATH)] + argv).returncode
     backend = args.backend or ("hip" if torch.cuda.is_available() else "cpu")
     compat = args.compat or {"mpi": "mpi", "cuda": "cuda"}.get(args.naming, "none")
     cfg = HeatConfig(nx=args.nx, ny=args.ny, steps=args.steps, cx=args.cx, cy=args.cy,
@@ -80,6 +93,9 @@ def main(argv=None) -> int:
     if root and args.naming == "mpi":
         out.write(report.mpi_banner(info.world, cfg.nx, cfg.ny, cfg.steps, cfg.converge))
         out.flush()
+    if args.port and args.transport == "tcp":
+        import os
+        os.environ["MASTER_PORT"] = str(args.port - 1)  # make_comm uses MASTER_PORT + 1
     solver = HeatSolver(cfg, transport=args.transport, dist_info=info)
     if args.resume:
         solver.load(args.resume)

@@ -83,12 +83,17 @@ class HeatSolver:
 
     def __init__(self, config: HeatConfig, transport: str = "auto",
                  dist_info: Optional[pcomm.DistInfo] = None, device: Optional[int] = None,
-                 hub: Optional[pcomm.LoopbackHub] = None, group=None):
+                 hub: Optional[pcomm.LoopbackHub] = None, group=None,
+                 shared: Optional[pcomm.EngineTransport] = None):
+        """`shared`: an existing EngineTransport (e.g. the run's one RCCL
+        communicator) instead of building a new transport."""
         self.config = config
         config.validate()
         if config.backend == "hip":
             _native.require_gpu_native()
         self.dist = dist_info or pcomm.env_info()
+        if shared is not None:
+            transport = shared.kind
         if transport == "auto":
             if self.dist.world == 1:
                 transport = "local"
@@ -106,12 +111,17 @@ class HeatSolver:
                 device = -1
         self.device = device
         self.transport = transport
-        self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0),
-                                                 hub=hub, group=group)
         params = config.to_native(device=device)
         h = ctypes.c_void_p()
-        _native.call("heat_solver_create", ctypes.byref(params), ctypes.byref(self._comm),
-                     ctypes.byref(h))
+        if shared is not None:
+            self._comm, self._keep = None, shared
+            _native.call("heat_solver_create_shared", ctypes.byref(params), shared.handle,
+                         ctypes.byref(h))
+        else:
+            self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0),
+                                                     hub=hub, group=group)
+            _native.call("heat_solver_create", ctypes.byref(params), ctypes.byref(self._comm),
+                         ctypes.byref(h))
         self._h = h
         self.info = self._info()
 

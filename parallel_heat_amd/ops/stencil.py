@@ -12,8 +12,9 @@ Reference kernels: ``heat`` (``cuda/cuda_heat.cu:140-163``) and the fused
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass
-from typing import Optional, Sequence, Tuple
+import enum
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
@@ -22,6 +23,56 @@ from ..models.config import INIT_MODES
 from ..parallel.topology import layout
 
 Box = Tuple[int, int, int, int]  # (r0, r1, c0, c1) in local coordinates
+
+
+class TbVariant(enum.IntFlag):
+    """Variant flags of the temporally blocked kernel (``heat::gpu::tbv`` in
+    csrc/include/heat/kernels.hpp).  The low two bits pick the register
+    pipeline; the rest pick the build and the launch layout."""
+    RING3 = 0             # 3-row rings, skew 1
+    RING4 = 1             # 4-row rings, skew 2
+    RING2 = 2             # 2-row rings + copy
+    RAMP = 3              # 3-row rings + compile-time ramp skip
+    SCALAR = 4            # scalar row-update build (depth 12 lives here)
+    XCD_GROUPS = 16       # contiguous wave ranges per XCD
+    ALT_DIRECTION = 32    # odd chunks stream bottom-up
+    FLOAT2 = 64           # float2 lanes (128-column strips)
+    FORCE_AGE_PAIRS = 256  # age groups even at equal weights
+    DIAG_NO_STORE = 1024  # diagnostics: no output stores (wrong results)
+    SPLIT = 2048          # two-wave level-split pipelines (depths 8, 12)
+    DIAG_CACHED_ROWS = 4096  # diagnostics: cache-resident input rows (wrong results)
+    NO_AGE_PAIRS = 16384  # never age-group
+    LINEAR = 32768        # balanced plan: equal strip-rows per unit
+    DEFAULT = RAMP | SCALAR | XCD_GROUPS       # 23
+    DEFAULT_DEEP = DEFAULT | SPLIT             # 2071
+
+
+@dataclass
+class TbTuning:
+    """Launch-planner knobs (``heat::gpu::TbTuning``); HEAT_TB_* environment
+    variables seed them when the library is first used."""
+    variant: int = -1
+    rounds: int = 0
+    min_len: int = 0
+    waves: int = 0
+    edge_frac: float = 1.0
+    age_weights: List[float] = field(default_factory=list)
+
+
+def tb_tuning() -> TbTuning:
+    t = _native.HeatTbTuning()
+    _native.call("heat_tb_get_tuning", ctypes.byref(t))
+    return TbTuning(t.variant, t.rounds, t.min_len, t.waves, t.edge_frac,
+                    [t.weights[i] for i in range(t.n_weights)])
+
+
+def set_tb_tuning(t: TbTuning) -> None:
+    n = len(t.age_weights)
+    if n > 4:
+        raise ValueError("at most 4 age weights")
+    c = _native.HeatTbTuning(int(t.variant), int(t.rounds), int(t.min_len), int(t.waves),
+                             float(t.edge_frac), n, 0, (ctypes.c_double * 4)(*t.age_weights))
+    _native.call("heat_tb_set_tuning", ctypes.byref(c))
 
 
 @dataclass
@@ -151,14 +202,13 @@ def mfma_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
 
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
-            waves_target: int = 0, variant: int = -1) -> None:
+            waves_target: int = 0, variant: int = -1, res_level: int = 0) -> None:
     """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes.
 
-    variant: -1 default (23 at depth <= 8, 2071 at depth 12); bits 0-1 pipeline
-    (0 ring-3, 1 ring-4 skew-2, 2 ring-2 + copy, 3 ring-3 + ramp), bit 2 the scalar
-    build, 16 XCD-grouped blocks, 32 odd chunks bottom-up, 64 float2 lanes,
-    256 age-paired chunks, 2048 two-wave level-split pipelines (depths 8/12),
-    diagnostics (wrong results): 1024 no stores, 4096 cache-resident input rows.
+    variant: -1 = chosen per launch (TbVariant.DEFAULT, or DEFAULT_DEEP for
+    large depth-12 launches); otherwise TbVariant flags.  res_level: the
+    residual (resid given) is max|u_l - u_(l-1)| after step l = res_level of
+    the pass (0 = depth).
     """
     if src.device.type == "cpu":
         raise ValueError("tb_step is a GPU kernel")
@@ -172,7 +222,7 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
     _native.call("heat_op_tb_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
                  src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy, arr,
                  len(boxes), depth, ctypes.c_void_p(rp) if rp else None,
-                 ctypes.c_void_p(_stream()), waves_target, variant)
+                 ctypes.c_void_p(_stream()), waves_target, int(variant), int(res_level))
 
 
 def tb_stamps(buf: Optional[torch.Tensor]) -> None:

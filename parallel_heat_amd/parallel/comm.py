@@ -214,3 +214,48 @@ def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = 
     else:
         raise ValueError(f"unknown transport {kind!r}")
     return comm, keep
+
+
+class EngineTransport:
+    """One native transport that several solvers use in turn.
+
+    ``bench.py``'s multi-GPU autotune builds a solver per candidate layout;
+    with a shared transport they all ride ONE RCCL communicator (one
+    ncclCommInitRank per rank per run, its P2P connections made once) instead
+    of one per candidate.  Collective: every rank constructs it with the same
+    kind.  Each solver keeps its own reference to the native object, so
+    ``close()`` is safe while solvers are alive."""
+
+    def __init__(self, kind: str, info: DistInfo, device: int = 0, hub: Optional[LoopbackHub] = None,
+                 group=None):
+        self.kind = kind
+        self.device = device
+        self._comm, self._keep = make_comm(kind, info, device=device, hub=hub, group=group)
+        h = ctypes.c_void_p()
+        _native.call("heat_transport_create", ctypes.byref(self._comm), ctypes.byref(h))
+        self.handle = h
+
+    def info(self) -> dict:
+        """The transport's own view: for RCCL ncclCommCount / ncclCommCuDevice /
+        ncclCommUserRank and the device's PCI bus id."""
+        i = _native.HeatTransportInfo()
+        _native.call("heat_transport_info_get", self.handle, ctypes.byref(i))
+        return {"name": i.name.decode(), "nranks": i.nranks, "device": i.device,
+                "user_rank": i.user_rank, "bus_id": i.bus_id.decode()}
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            _native.call("heat_transport_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -14,7 +14,7 @@ ranks), and returns the fastest configuration plus the measured table.
     solver = HeatSolver(best, dist_info=info)
 
 Every rank must call it with the same arguments (it builds and destroys one
-solver per candidate, i.e. one RCCL communicator each).  A candidate the
+solver per candidate; with ``shared`` they all use one RCCL communicator).  A candidate the
 engine rejects (e.g. a block thinner than its halo) is skipped on every rank
 (the rejection is decided from global quantities, so all ranks agree).
 """
@@ -67,14 +67,20 @@ def describe(cfg: HeatConfig, world: int) -> Dict[str, object]:
 
 
 def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConfig]] = None,
-             steps: int = 1000, repeats: int = 2,
+             steps: int = 1000, repeats: int = 3,
              make: Optional[Callable[[HeatConfig], object]] = None,
-             log: Optional[Callable[[str], None]] = None) -> Tuple[HeatConfig, List[dict]]:
+             log: Optional[Callable[[str], None]] = None,
+             shared=None) -> Tuple[HeatConfig, List[dict]]:
     """Time every candidate (steps x repeats, after one untimed run of `steps`
     that captures the graphs) and return (fastest config, table).
 
-    `make(cfg)` builds the solver (default: HeatSolver(cfg, dist_info=info)).
-    Collective over torch.distributed's default group when info.world > 1."""
+    `make(cfg)` builds the solver (default: HeatSolver(cfg, dist_info=info,
+    shared=shared)); pass `shared` (a parallel.comm.EngineTransport) so every
+    candidate rides the same communicator instead of one ncclCommInitRank per
+    candidate.  Collective over torch.distributed's default group when
+    info.world > 1: every rank takes the same sequence of agreements, so a
+    candidate that fails on any rank (construction or run) is skipped on all
+    of them together instead of leaving the ranks in mismatched collectives."""
     import torch
     import torch.distributed as dist
 
@@ -85,7 +91,7 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
         candidates = default_candidates(cfg, world)
     if make is None:
         def make(c):
-            return HeatSolver(c, dist_info=info)
+            return HeatSolver(c, dist_info=info, shared=shared)
 
     gpu = cfg.backend == "hip"
 
@@ -95,6 +101,9 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
         t = torch.tensor([flag], dtype=torch.float64, device="cuda" if gpu else "cpu")
         dist.all_reduce(t, op=op)
         return float(t.item())
+
+    MIN = dist.ReduceOp.MIN if world > 1 else None
+    MAX = dist.ReduceOp.MAX if world > 1 else None
 
     def sync():
         if gpu:
@@ -115,7 +124,7 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
         except _native.NativeError as e:
             ok = 0.0
             row["error"] = str(e).splitlines()[0][:200]
-        if agree_all(ok, dist.ReduceOp.MIN if world > 1 else None) < 1.0:
+        if agree_all(ok, MIN) < 1.0:
             if solver is not None:
                 solver.close()
             row.setdefault("error", "rejected on another rank")
@@ -123,22 +132,35 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             if log:
                 log(f"autotune: {row} skipped")
             continue
+        dt = 0.0
         try:
-            solver.run(steps)  # graph capture, RCCL connections
-            barrier()
-            sync()
-            t0 = time.perf_counter()
-            for _ in range(repeats):
-                solver.run(steps)
-            sync()
-            barrier()
-            dt = agree_all(time.perf_counter() - t0, dist.ReduceOp.MAX if world > 1 else None)
-            row["halo"] = solver.info.halo
-            row["tb_depth"] = solver.info.tb_depth
+            try:
+                solver.run(steps)  # graph capture, RCCL connections
+                barrier()
+                sync()
+                t0 = time.perf_counter()
+                for _ in range(repeats):
+                    solver.run(steps)
+                sync()
+                dt = time.perf_counter() - t0
+                row["halo"] = solver.info.halo
+                row["tb_depth"] = solver.info.tb_depth
+                ok = 1.0
+            except _native.NativeError as e:
+                ok = 0.0
+                row["error"] = str(e).splitlines()[0][:200]
         finally:
             solver.close()
+        if agree_all(ok, MIN) < 1.0:
+            row.setdefault("error", "failed on another rank")
+            table.append(row)
+            if log:
+                log(f"autotune: {row} failed")
+            continue
+        dt = agree_all(dt, MAX)
         ms = dt * 1e3 * 1000.0 / (steps * repeats)
         row["ms_per_1000_iters"] = round(ms, 4)
+        row["repeats"] = repeats
         table.append(row)
         if log:
             log(f"autotune: {row}")

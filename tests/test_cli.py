@@ -190,3 +190,52 @@ def test_cli_memory_plan(tmp_path):
     huge = json.loads(heat(["--nx", "600000", "--ny", "600000", "--gpus", "8", "--plan"],
                            tmp_path).stdout)
     assert not huge["fits_288gb"]
+
+
+def _flags_of(text):
+    import re
+    return set(re.findall(r"(?<![\w-])(--[a-z][a-z0-9-]*)", text))
+
+
+def test_cli_flag_parity():
+    # The two front ends accept the same flags (SURVEY §5 config system; the
+    # reference's -D macros, mpi/Makefile:12-22).  Help flags aside, the only
+    # difference allowed is a VALUE: --transport torch is Python-only.
+    native = heat(["--help"], ROOT).stdout
+    from parallel_heat_amd.cli import build_parser
+    py = {o for a in build_parser()._actions for o in a.option_strings if o.startswith("--")}
+    nat = _flags_of(native)
+    assert nat - py == set(), f"native-only flags: {sorted(nat - py)}"
+    assert py - nat - {"--help"} == set(), f"python-only flags: {sorted(py - nat - {'--help'})}"
+
+
+@pytest.mark.parametrize("args", [
+    ["--nx", "20", "--ny", "20", "--steps", "100", "--naming", "mpi"],
+    ["--nx", "24", "--ny", "30", "--steps", "10000", "--converge", "--naming", "mpi"],
+    ["--nx", "24", "--ny", "30", "--steps", "10000", "--converge", "--naming", "cuda"],
+    ["--nx", "17", "--ny", "23", "--steps", "40", "--init", "random", "--seed", "3",
+     "--out-format", "checksum", "--out", "c.json"],
+])
+def test_cli_reference_lines_match(tmp_path, args):
+    import re
+    # Identical reference lines and identical output files from both CLIs
+    # (elapsed-time values aside).
+    outs = {}
+    for name, cmd in (("native", [HEAT]), ("python", [sys.executable, "-m", "parallel_heat_amd"])):
+        d = tmp_path / name
+        d.mkdir()
+        p = subprocess.run(cmd + ["--backend", "cpu"] + args, cwd=d, capture_output=True,
+                           text=True, timeout=300, check=True,
+                           env=dict(os.environ, PYTHONPATH=ROOT))
+        lines = [re.sub(r"[0-9.]+ (m?secs)", r"T \1", l) if l.startswith("Elapsed time") else l
+                 for l in p.stdout.splitlines()]
+        files = {f.name: f.read_bytes() for f in sorted(d.iterdir())}
+        outs[name] = (lines, files)
+    assert outs["native"][0] == outs["python"][0]
+    assert outs["native"][1].keys() == outs["python"][1].keys()
+    for k, v in outs["native"][1].items():
+        if k.endswith(".json"):
+            a, b = json.loads(v), json.loads(outs["python"][1][k])
+            assert a["hash"] == b["hash"] and a["step"] == b["step"]
+        else:
+            assert v == outs["python"][1][k], k

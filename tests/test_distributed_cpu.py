@@ -110,3 +110,17 @@ def test_autotune_collective_gloo(tmp_path):
     assert layouts == {(4, 1), (2, 2)}
     assert len(res["table"]) == 6
     assert all(r["ms_per_1000_iters"] > 0 for r in res["table"])
+
+
+def test_autotune_shared_transport_gloo(tmp_path):
+    # bench.py's multi-GPU path: ONE engine transport per rank for every
+    # autotune candidate and the final solver (one communicator per run).
+    from .dist_worker import run_tune
+
+    kw = dict(nx=40, ny=36, steps=0, init="random", seed=5, backend="cpu", tb_depth=2)
+    res = run_tune(2, kw, tmp_path, transport="shared")
+    assert all(c == res["choices"][0] for c in res["choices"])
+    assert all(r["ms_per_1000_iters"] > 0 for r in res["table"])
+    got = np.load(str(tmp_path / f"tune_2_{__import__('os').getpid()}.json") + ".npy")
+    ref, _ = single(kw, 29)
+    assert np.array_equal(got, ref)

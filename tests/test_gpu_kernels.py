@@ -9,6 +9,11 @@ from parallel_heat_amd.models import reference as R
 
 pytestmark = pytest.mark.gpu
 
+V = ops.TbVariant
+RAMP_S = V.RAMP | V.SCALAR            # 7: scalar ring-3 + ramp
+DEF = V.DEFAULT                       # 23: + XCD groups
+DEEP = V.DEFAULT_DEEP                 # 2071: + two-wave level-split pipelines
+
 
 def _fields(lx, ly, halo, dev, nx=None, ny=None, gx0=0, gy0=0, mode="random", seed=3):
     nx = nx or lx
@@ -49,10 +54,13 @@ def test_naive_step_vs_torch(gpu):
     torch.testing.assert_close(b.owned(), ref, rtol=1e-6, atol=1e-4)
 
 
-# 0/3 packed ring-3 (+ramp), 4/7 scalar; +16 XCD-grouped blocks, +32 odd
-# chunks streamed bottom-up (mirrored rows, incl. the plate's top/bottom rows);
-# +64 float2 lanes (128-column strips).
-@pytest.mark.parametrize("variant", [0, 3, 4, 7, 23, 39, 55, 71, 87, 119])
+# Packed ring-3 (+ramp), scalar; + XCD-grouped blocks, + odd chunks streamed
+# bottom-up (mirrored rows, incl. the plate's top/bottom rows); + float2
+# lanes (128-column strips).
+@pytest.mark.parametrize("variant", [V.RING3, V.RAMP, V.SCALAR, RAMP_S, DEF,
+                                     RAMP_S | V.ALT_DIRECTION, DEF | V.ALT_DIRECTION,
+                                     RAMP_S | V.FLOAT2, DEF | V.FLOAT2,
+                                     DEF | V.FLOAT2 | V.ALT_DIRECTION])
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     lx, ly = 203, 517  # odd sizes: partial strips and chunks
@@ -64,9 +72,11 @@ def test_tb_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant,depth", [(7, 12), (23, 12), (55, 12), (279, 12),
-                                           (2055, 8), (2071, 8), (2071, 12), (2103, 12),
-                                           (2327, 12)])
+@pytest.mark.parametrize("variant,depth", [(RAMP_S, 12), (DEF, 12), (DEF | V.ALT_DIRECTION, 12),
+                                           (DEF | V.FORCE_AGE_PAIRS, 12),
+                                           (RAMP_S | V.SPLIT, 8), (DEEP, 8), (DEEP, 12),
+                                           (RAMP_S | V.SPLIT | V.ALT_DIRECTION, 12),
+                                           (DEEP | V.FORCE_AGE_PAIRS, 12)])
 def test_tb_deep_bitwise_vs_cpu_oracle(gpu, depth, variant):
     # Depth 12 exists in the scalar ring-3+ramp build only (+32 mirrored odd
     # chunks, +256 age pairs); +2048: two-wave level-split pipelines
@@ -80,7 +90,8 @@ def test_tb_deep_bitwise_vs_cpu_oracle(gpu, depth, variant):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant", [263, 279, 311])  # +256: age-paired chunks forced
+@pytest.mark.parametrize("variant", [V.FORCE_AGE_PAIRS | RAMP_S, V.FORCE_AGE_PAIRS | DEF,
+                                     V.FORCE_AGE_PAIRS | DEF | V.ALT_DIRECTION])
 @pytest.mark.parametrize("depth", [3, 8, 12])
 @pytest.mark.parametrize("waves", [0, 64, 1000, 4096])
 def test_tb_age_pairs_bitwise(gpu, depth, variant, waves):
@@ -96,7 +107,7 @@ def test_tb_age_pairs_bitwise(gpu, depth, variant, waves):
     assert torch.equal(got, ref), f"max diff {(got - ref).abs().max()}"
 
 
-@pytest.mark.parametrize("variant", [7, 55, 87, 2071])
+@pytest.mark.parametrize("variant", [RAMP_S, DEF | V.ALT_DIRECTION, DEF | V.FLOAT2, DEEP])
 @pytest.mark.parametrize("waves", [64, 4096])
 def test_tb_chunking_invariance(gpu, waves, variant):
     lx, ly, k = 300, 1000, 8
@@ -127,13 +138,13 @@ def test_tb_subdomain_offsets_and_boxes(gpu):
     d = ops.Field(lx, ly, 8, gpu)
     ops.init_field(c, g, "random", 5)
     ops.init_field(d, g, "random", 5)
-    ops.tb_step(c, d, g, 8, boxes=[(0, lx, 0, 296), (0, lx, 296, ly)], variant=2071)
+    ops.tb_step(c, d, g, 8, boxes=[(0, lx, 0, 296), (0, lx, 296, ly)], variant=DEEP)
     torch.cuda.synchronize()
     full8 = _cpu_steps(ops.Geom(nx=NX, ny=NY), NX, NY, 1, 8, seed=5)
     assert torch.equal(d.owned().cpu(), full8[ox:ox + lx, oy:oy + ly])
 
 
-@pytest.mark.parametrize("k,variant", [(4, -1), (8, 2071), (12, 2071)])
+@pytest.mark.parametrize("k,variant", [(4, -1), (8, DEEP), (12, DEEP)])
 def test_tb_residual(gpu, k, variant):
     lx, ly = 64, 300
     g, a, b = _fields(lx, ly, k, gpu)
@@ -143,6 +154,43 @@ def test_tb_residual(gpu, k, variant):
     prev = _cpu_steps(g, lx, ly, k, k - 1)
     last = _cpu_steps(g, lx, ly, k, k)
     assert ops.resid_value(resid) == float((last - prev).abs().max())
+
+
+@pytest.mark.parametrize("k,variant,lx", [(12, DEEP, 700), (12, DEF, 203), (8, DEEP, 500),
+                                          (8, V.RING3, 203), (5, V.RAMP, 203),
+                                          (12, DEF | V.ALT_DIRECTION, 900)])
+def test_tb_residual_at_inner_level(gpu, k, variant, lx):
+    # A convergence check inside a pass: the residual after step l of the
+    # pass (both stages of the split pipeline, the ramp, the main loop and the
+    # mirrored chunks), the output unchanged.
+    ly = 517
+    g, a, b = _fields(lx, ly, k, gpu)
+    levels = [_cpu_steps(g, lx, ly, k, j) for j in range(k + 1)]
+    for lvl in sorted({1, 2, k // 2, k // 2 + 1, k - 1, k}):
+        resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+        ops.tb_step(a, b, g, k, resid=resid, variant=variant, waves_target=512, res_level=lvl)
+        torch.cuda.synchronize()
+        want = float((levels[lvl] - levels[lvl - 1]).abs().max())
+        assert ops.resid_value(resid) == want, (lvl, ops.resid_value(resid), want)
+        assert torch.equal(b.owned().cpu(), levels[k])
+
+
+@pytest.mark.parametrize("k,variant", [(8, DEF), (12, DEF), (8, DEEP), (12, DEEP)])
+def test_tb_multi_pass_vs_torch_fp32(gpu, k, variant):
+    # The direct anchor: K passes of the hot kernel against K*k applications
+    # of the plain PyTorch fp32 stencil (R.step_torch) on the GPU, tolerance
+    # growing with the step count (FMA contraction differs from torch's).
+    lx, ly, passes = 600, 777, 5
+    g, a, b = _fields(lx, ly, k, gpu)
+    u = a.owned().clone().float()
+    for _ in range(passes):
+        ops.tb_step(a, b, g, k, variant=variant)
+        a, b = b, a
+    for _ in range(passes * k):
+        u = R.step_torch(u)
+    torch.cuda.synchronize()
+    n = passes * k
+    torch.testing.assert_close(a.owned(), u, rtol=2e-6 * n, atol=1e-5 * n)
 
 
 def test_residual_and_pack_unpack(gpu):

@@ -11,7 +11,10 @@ import os
 import statistics
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# HEAT_PY_ROOT: import another copy of the package (e.g. a previous build,
+# for an A/B in one session).
+sys.path.insert(0, os.environ.get("HEAT_PY_ROOT") or
+                os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
