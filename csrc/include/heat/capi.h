@@ -159,8 +159,7 @@ int heat_op_tb_stamps(void* buf, int64_t waves);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,
-                    int variant /* -1 default; heat::gpu::tbv flags */,
-                    int res_level /* residual after this step of the pass; 0 = depth */);
+                    int variant /* -1 default; heat::gpu::tbv flags */);
 /* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares. */
 typedef struct heat_tb_tuning {
   int32_t variant, rounds, min_len, waves;

@@ -55,7 +55,9 @@ enum : int {
   kSplit = 2048,        // two-wave level-split pipelines (tbx; depths 8, 12)
   kDiagCachedRows = 4096,  // diagnostics: cache-resident input rows (wrong results)
   kNoAgePairs = 16384,  // never age-group (A/B of the weights)
-  kLinear = 32768,      // balanced linear plan (equal strip-rows per unit)
+  kLinear = 32768,      // force the balanced linear plan (equal strip-rows per unit)
+  kNoLinear = 65536,    // never switch to it (by default it replaces a classic
+                        // plan that fills < 90 % of the launch's units)
   // Defaults: depth <= 8 and small launches at 12; large launches at 12.
   kDefault = kRamp | kScalar | kXcdGroups,  // 23
   kDefaultDeep = kDefault | kSplit,         // 2071
@@ -114,12 +116,8 @@ void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box
 void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                unsigned* resid, hipStream_t st);
 
-// `res_level` (1..depth, 0 = depth): the fused residual (resid != null) is
-// max|level res_level - level res_level-1| -- a convergence check inside the
-// pass.
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1,
-             int res_level = 0);
+             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
 // Variant a launch of `depth` uses by default (HEAT_TB_VARIANT overrides).
 int tb_default_variant(int depth);
 // Variant tb_step picks for a launch of `depth` with this much work

@@ -114,8 +114,8 @@ class Solver {
   float* current() { return field_[cur_]; }
 
  private:
-  // One pass of a segment: k steps, with the convergence residual taken
-  // after step rl of the pass (1..k; 0 = no check in this pass).
+  // One pass of a segment: k steps; rl = k: the pass ends at a check (its
+  // last level carries the residual), 0: no check.
   struct PassPlan {
     int k = 0;
     int rl = 0;
@@ -133,8 +133,8 @@ class Solver {
   void free_all();
   void init_fields();
   std::vector<int> pass_depths(int64_t n) const;
-  // Passes for steps [step0, step0+n) with a residual level at every check
-  // point (device-gated runs: a check may fall inside a TB pass).
+  // Passes for steps [step0, step0+n), cut at every check point (the
+  // residual is the last level of its pass).
   std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;
   void enqueue_segment(const std::vector<PassPlan>& plan);
   void enqueue_pass(int k, int rl);
@@ -158,9 +158,7 @@ class Solver {
   // segment; returns its pass records and check steps relative to step_.
   void launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_t phase,
                       bool use_graph, std::vector<PassRec>* recs, std::vector<int64_t>* checks);
-  // Re-run rl single steps from field_[cur] (the source of a pass that
-  // overshot the converging check) with the LDS kernel, ungated.
-  void replay_steps(int cur, int rl);
+
   void reduce_scalars(double* f64, int nf, uint64_t* u64, int nu, float* fmax, int nm);
 
   Params P_;

@@ -421,11 +421,8 @@ void tb_set_stamps(unsigned long long* buf, int64_t waves) {
 }
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
-             int res_level) {
+             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
-  if (res_level <= 0) res_level = depth;
-  HEAT_CHECK(res_level <= depth, "residual level %d of a depth-%d pass", res_level, depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   const TbTuning tune = tb_tuning();
   if (variant < 0) {
@@ -498,7 +495,6 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.src = src;
   args.dst = dst;
   args.resid = resid;
-  args.res_level = res_level;
   args.g = g;
   args.flags = ((variant & tbv::kXcdGroups) ? tbdetail::kTbXcdGroups : 0) |
                ((variant & tbv::kAltDirection) ? tbdetail::kTbAltDirection : 0) |
@@ -573,12 +569,32 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       add(bot, edge_len);
     }
   };
-  if (variant & tbv::kLinear) {
+  bool linear = variant & tbv::kLinear;
+  if (!linear) {
+    // Keep the total within waves_target (whole resident rounds): a few extra
+    // waves would form a nearly empty extra round.
+    plan(len);
+    for (int it = 0; it < 8 && waves > waves_target; ++it) {
+      len = std::max(len + 1, ceil_div(len * int64_t(waves), int64_t(waves_target)));
+      plan(len);
+    }
+    // Few long chunks per strip quantise badly: 565 strips x 131072 rows
+    // (131072^2 on one GPU, or a 16384-row slab of it) became 1130 two-wave
+    // pipelines for 2048 slots, 2.25 blocks per CU, every chunk touching the
+    // plate's top or bottom row (masked path).  Balanced linear plans ran
+    // those at 5.16 / 4.65 Tcells/s instead of 3.50 / 4.33; at 8192^2 (the
+    // classic plan fills 98 %) they lose 24 %: units that cross a strip end
+    // or split off the masked edge rows pay a second pipeline ramp, and in a
+    // one-round launch the slowest unit sets the time
+    // (profiles/r3_linear_plans.md).
+    linear = !(variant & tbv::kNoLinear) && waves < (9 * int64_t(waves_target)) / 10 &&
+             total_strip_rows >= 32 * int64_t(depth) * waves_target;
+  }
+  if (linear) {
     // Balanced plan: the boxes as one strip-row sequence cut into equal
     // ranges, one per unit (per group of G units with age pairs), so every
-    // unit -- and every SIMD -- gets the same rows whatever the shape.  The
-    // classic (strip, chunk) plan quantises: e.g. 565 strips x 131072 rows
-    // gave 1130 two-wave pipelines for 2048 slots, 2.25 blocks per CU.
+    // unit -- and every SIMD -- gets the same rows whatever the shape.
+    n = 0;
     int64_t total = 0;
     for (int b = 0; b < nbox; ++b) {
       const Box& B = boxes[b];
@@ -604,14 +620,6 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     args.lin_total = total;
     args.lin_slack = 2 * int64_t(depth);
     args.flags |= tbdetail::kTbLinear;
-  } else {
-    // Keep the total within waves_target (whole resident rounds): a few extra
-    // waves would form a nearly empty extra round.
-    plan(len);
-    for (int it = 0; it < 8 && waves > waves_target; ++it) {
-      len = std::max(len + 1, ceil_div(len * int64_t(waves), int64_t(waves_target)));
-      plan(len);
-    }
   }
   if (n == 0) return;
   args.nbox = n;

@@ -37,10 +37,6 @@ struct TbArgs {
   // strip<<32 | chunk, 4 u64
   // per wave index; see tb_set_stamps().
   unsigned long long* stamps;
-  // The fused residual (resid != null) is max|level res_level - level
-  // res_level-1| over the output boxes (1..depth; a convergence check that
-  // falls inside the pass).
-  int res_level;
   // Linear plans (kTbLinear): total strip-rows of the boxes and the slack
   // (rows) within which a unit boundary moves to a strip end.
   int64_t lin_total;

@@ -181,14 +181,8 @@ struct TbStream {
   vecf R[K][RING];  // R[s][slot]: rows of level s (level 0 = input rows; LAG 3: s >= 1)
   vecf P[PF];       // prefetch ring (input row i + PF; LAG 0-2)
   vecf L0[LAG == 3 ? 6 : 1];  // LAG 3: level-0 rows t-2 .. t+3 (see lv())
-  unsigned m = 0;
+  float m = 0.f;  // residual max |delta| (RES)
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
-  // RES: the residual is taken at this stage's level res_lv (1..K; 0 = not
-  // in this stage) over output rows [qb, qe) -- a convergence check inside
-  // the pass (levels < K) or at its end (K).
-  int res_lv = K;
-  int64_t qb = 0, qe = 0;
-  bool res_lane = false;  // this lane's columns are output columns of the strip
   // src / dst (run() arguments) point at the strip's first column, the same
   // for every lane (scalar registers); lane l adds lo = V * l elements, so
   // loads and stores use the scalar-base + 32-bit lane-offset addressing
@@ -266,21 +260,18 @@ struct TbStream {
     }
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
-    }
-  }
-
-  // Residual of level s, row `row` (out = the new row, b = its level s-1
-  // centre row).  s is a compile-time constant once the level loops are
-  // unrolled and res_lv / row are wave-uniform, so in the RES instantiation
-  // this costs two scalar compares per level and row; the |delta| max runs
-  // for one level only.  Columns past the box end (the last lane's spill
-  // into padding or stale ghost columns) are written but not counted.
-  __device__ __forceinline__ void res_at(int s, int64_t row, const vecf& out, const vecf& b) {
-    if constexpr (RES) {
-      if (s == res_lv && row >= qb && row < qe && res_lane) {
+      if constexpr (RES) {
+        // max |delta| with the NaN-propagating IEEE-2019 maximum
+        // (v_maximum3_f32, abs folded into its inputs): a NaN or inf
+        // anywhere reaches the judge.  Columns past the box end (the last
+        // lane's spill into padding or stale ghost columns) are written but
+        // not counted.
+        float d[V];
 #pragma unroll
-        for (int j = 0; j < V; ++j)
-          m = max(m, (j == 0 || rc > j) ? __float_as_uint(fabsf(out[j] - b[j])) : 0u);
+        for (int j = 0; j < V; ++j) d[j] = (j == 0 || rc > j) ? __builtin_fabsf(out[j] - b[j]) : 0.f;
+#pragma unroll
+        for (int j = 0; j < V; j += 2)
+          m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(d[j], d[j + 1]));
       }
     }
   }
@@ -305,7 +296,6 @@ struct TbStream {
         const int64_t row = i - s - 1;  // row of level s+1 computed now
         const bool ok = !ROWCHK || row_in(row, rlo, rhi);
         const vecf cn = upd(R[s][sa], R[s][sb], c, ok);
-        res_at(s + 1, row, cn, R[s][sb]);
         if (s == K - 1) emit(cn, R[s][sb], row, dst, pitch, rb, re, store_lane);
         R[s][sa] = c;  // level s row i-s replaces the consumed row i-s-2
         c = cn;
@@ -322,7 +312,6 @@ struct TbStream {
         R[s][modn<RING>(U - rs)] = upd(R[s - 1][modn<RING>(U - rs - 1)],
                                        R[s - 1][modn<RING>(U - rs)],
                                        R[s - 1][modn<RING>(U - rs + 1)], ok);
-        res_at(s, i - rs, R[s][modn<RING>(U - rs)], R[s - 1][modn<RING>(U - rs)]);
       }
       const int rK = STEP * K;
       const int64_t ro = i - rK;  // output row of this iteration
@@ -330,7 +319,6 @@ struct TbStream {
       const vecf& b = R[K - 1][modn<RING>(U - rK)];
       const vecf out =
           upd(R[K - 1][modn<RING>(U - rK - 1)], b, R[K - 1][modn<RING>(U - rK + 1)], ok);
-      res_at(K, ro, out, b);
       emit(out, b, ro, dst, pitch, rb, re, store_lane);
     }
   }
@@ -386,14 +374,12 @@ struct TbStream {
       const bool ok = !ROWCHK || row_in(i - s, rlo, rhi);
       lv(s, T6 - s) = HEAT_TB_UPD(s, lv(s - 1, T6 - s - 1), lv(s - 1, T6 - s),
                                   lv(s - 1, T6 - s + 1), ok);
-      res_at(s, i - s, lv(s, T6 - s), lv(s - 1, T6 - s));
     }
     const int64_t ro = i - K;  // output row of this iteration
     const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
     const vecf& b = lv(K - 1, T6 - K);
     const vecf out = HEAT_TB_UPD(K, lv(K - 1, T6 - K - 1), b, lv(K - 1, T6 - K + 1), ok);
 #undef HEAT_TB_UPD
-    res_at(K, ro, out, b);
     emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
   }
 
@@ -404,7 +390,6 @@ struct TbStream {
       if constexpr (2 * S <= T) {
         const bool ok = !ROWCHK || row_in(i - S, rlo, rhi);
         lv(S, T - S) = upd(lv(S - 1, T - S - 1), lv(S - 1, T - S), lv(S - 1, T - S + 1), ok);
-        res_at(S, i - S, lv(S, T - S), lv(S - 1, T - S));
       }
       ramp_levels<T, S + 1>(i, rlo, rhi, upd);
     }
@@ -547,7 +532,7 @@ __device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, 
 // the segment's first row, so consecutive segments of one unit keep the
 // ring protocol's numbers monotonic).  Returns this lane's residual max.
 template <int K, int LAG, int K1>
-__device__ __forceinline__ unsigned tb_segment(const TbArgs& a, const TbBox& bx, int strip,
+__device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, int strip,
                                                int chunk, int64_t rb, int64_t re, int stage,
                                                vecf* ring, unsigned* cnt, int64_t qoff) {
   constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
@@ -583,7 +568,7 @@ __device__ __forceinline__ unsigned tb_segment(const TbArgs& a, const TbBox& bx,
     rlo = int(max<int64_t>(M - hi, -(int64_t(1) << 30)));
     rhi = int(min<int64_t>(M - lo, int64_t(1) << 30));
   }
-  unsigned m = 0;
+  float m = 0.f;
   // Which Dirichlet mode this wave needs (all wave-uniform).
   const bool rows_in = gx_lo >= 1 && gx_hi <= g.nx - 2;
   const bool left = gy_lo < 1, right = gy_hi > g.ny - 2;
@@ -605,39 +590,25 @@ __device__ __forceinline__ unsigned tb_segment(const TbArgs& a, const TbBox& bx,
     } else if constexpr (MD >= 2) {
       upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
-    // Residual level (1..K) of the launch; with two stages each takes the
-    // levels it computes (0 = none in this stage).  Output rows [rb, re)
-    // map onto themselves under the bottom-up mirror.
-    const int rl = a.res_level;
     if constexpr (K1 == 0) {
       TbStream<K, LAG, MD, decltype(res_c)::value> st;
       st.lo = V * lane;
       st.rc = int(min<int64_t>(cend - col, V));
-      st.res_lv = rl;
-      st.qb = rb;
-      st.qe = re;
-      st.res_lane = store_lane;
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     } else if (stage == 0) {
       // Level-K1 rows [rb - K2, re + K2): exactly what stage 1's trapezoid reads.
-      TbStream<K1, LAG, MD, decltype(res_c)::value, 1> st;
+      TbStream<K1, LAG, MD, false, 1> st;
       st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
       st.seq0 = rb - K2;
       st.qoff = qoff;
-      st.rc = int(min<int64_t>(cend - col, V));
-      st.res_lv = rl <= K1 ? rl : 0;
-      st.qb = rb;
-      st.qe = re;
-      st.res_lane = store_lane;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
-      m = st.m;
     } else {
       TbStream<K2, LAG, MD, decltype(res_c)::value, 2> st;
       st.lo = V * lane;
@@ -646,10 +617,6 @@ __device__ __forceinline__ unsigned tb_segment(const TbArgs& a, const TbBox& bx,
       st.released = cnt + 1;
       st.qoff = qoff;
       st.rc = int(min<int64_t>(cend - col, V));
-      st.res_lv = rl > K1 ? rl - K1 : 0;
-      st.qb = rb;
-      st.qe = re;
-      st.res_lane = store_lane;
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
@@ -703,7 +670,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
   const int lane = threadIdx.x & 63;
   const bool pairs = a.flags & tbdetail::kTbAgePairs;
   const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  unsigned m = 0;
+  float m = 0.f;
   int strip = 0, chunk = wave;
   const bool linear = a.flags & tbdetail::kTbLinear;
   int64_t x0 = 0, x1 = 1;  // linear: this unit's strip-row range
@@ -762,11 +729,11 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       x0 = x1;  // one segment
       if (rb >= re) break;
     }
-    m = max(m, tb_segment<K, LAG, K1>(a, a.box[bi], strip, chunk, rb, re, stage, ring, cnt, qoff));
+    m = __builtin_elementwise_maximum(
+        m, tb_segment<K, LAG, K1>(a, a.box[bi], strip, chunk, rb, re, stage, ring, cnt, qoff));
     qoff += (re - rb) + 2 * K2;
   }
-  if (a.resid != nullptr && (K1 == 0 || (stage == 0) == (a.res_level <= K1)))
-    wave_max_atomic(m, a.resid);
+  if (a.resid != nullptr && (K1 == 0 || stage == 1)) wave_max_atomic(__float_as_uint(m), a.resid);
   if (a.stamps && lane == 0) {
     const int64_t idx = int64_t(wave) + int64_t(age) * a.total_waves;
     unsigned long long* st = a.stamps + 4 * (K1 == 0 ? idx : 2 * idx + stage);

@@ -443,15 +443,14 @@ int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, 
 
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes, int nbox,
-                    int depth, unsigned* resid, void* stream, int waves_target, int variant,
-                    int res_level) {
+                    int depth, unsigned* resid, void* stream, int waves_target, int variant) {
   return guard([&] {
     HEAT_CHECK(nbox >= 1 && nbox <= 5, "nbox %d", nbox);
     heat::Box b[5];
     for (int i = 0; i < nbox; ++i)
       b[i] = heat::Box{boxes[4 * i], boxes[4 * i + 1], boxes[4 * i + 2], boxes[4 * i + 3]};
     heat::gpu::tb_step(src, dst, geom(pitch, gx0, gy0, nx, ny, cx, cy), b, nbox, depth, resid,
-                       S(stream), waves_target, variant, res_level);
+                       S(stream), waves_target, variant);
   });
 }
 

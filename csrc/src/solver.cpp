@@ -284,46 +284,29 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
 }
 
 std::vector<Solver::PassPlan> Solver::plan_passes(int64_t step0, int64_t n) const {
-  // The pass depths of an unchecked segment, then a residual level at every
-  // check point.  A TB pass keeps its depth when one check falls inside it
-  // (the kernel takes the residual at that level; if the run converges
-  // there, replay_steps recomputes the check's state from the pass source,
-  // which no later, gated, pass overwrites).  A pass with two checks -- or a
-  // non-TB pass, whose single steps ping-pong over the source -- is cut at
-  // the first check and the rest re-split into supported depths.
-  const bool tb = tb_kernel();
+  // Segments end at check points, so every check is the last step of a pass
+  // and the kernel takes its residual at the pass's last level (emit time).
+  // A residual at an arbitrary inner level (one uniform branch per level and
+  // row) measured +33 % (split pipelines) / +57 % (single wave) per check
+  // pass at 8192^2 against +12 % / +1 % at the last level
+  // (profiles/r3_residual_cost.md): cutting passes at checks is cheaper.
   std::vector<PassPlan> out;
-  std::deque<int> todo;
-  for (int k : pass_depths(n)) todo.push_back(k);
   int64_t pos = step0;
-  auto push_rest = [&](int r) {
-    std::vector<int> parts;
-    while (r > 0) {
-      int d = std::min(r, T_);
-      if (tb)
-        while (!gpu::tb_depth_supported(d)) --d;
-      parts.push_back(d);
-      r -= d;
-    }
-    for (auto it = parts.rbegin(); it != parts.rend(); ++it) todo.push_front(*it);
-  };
-  while (!todo.empty()) {
-    const int k = todo.front();
-    todo.pop_front();
-    const int64_t c = P_.converge ? next_check_after(pos) : INT64_MAX;
-    if (c > pos + k) {
-      out.push_back({k, 0});
-    } else {
-      const int k1 = int(c - pos);
-      const bool second = next_check_after(c) <= pos + k;
-      if (k1 == k || (tb && !second)) {
-        out.push_back({k, k1});
-      } else {
-        out.push_back({k1, k1});
-        push_rest(k - k1);
+  const int64_t end = step0 + n;
+  while (pos < end) {
+    int64_t seg = end - pos;
+    bool check = false;
+    if (P_.converge) {
+      const int64_t c = next_check_after(pos);
+      if (c <= end) {
+        seg = c - pos;
+        check = true;
       }
     }
-    pos += out.back().k;
+    const auto d = pass_depths(seg);
+    for (size_t i = 0; i < d.size(); ++i)
+      out.push_back({d[i], check && i + 1 == d.size() ? d[i] : 0});
+    pos += seg;
   }
   return out;
 }
@@ -505,7 +488,7 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
   }
 
   if (!split) {
-    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target, -1, rl);
+    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target);
     return;
   }
   // Boundary bands are `band` >= k deep (k for exchange-first; H for the
@@ -517,10 +500,10 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
   const int64_t c1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
   if (part == 0) {
     Box in{r0, r1, c0, c1};
-    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target, -1, rl);
+    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target);
   } else {
     Box b[4] = {{0, r0, 0, ly}, {r1, lx, 0, ly}, {r0, r1, 0, c0}, {r0, r1, c1, ly}};
-    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target, -1, rl);
+    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target);
     // cur_ flips once per pass, after the boundary part.
   }
 }
@@ -867,33 +850,6 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
   *checks = it->second.checks;
 }
 
-void Solver::replay_steps(int cur, int rl) {
-  // rl single LDS-kernel steps from field_[cur], ungated, over the owned
-  // block grown by the steps still to come on sides with a neighbour (the
-  // source's ghosts are valid that deep: the overshooting pass read k > rl
-  // of them).  Bitwise the same arithmetic as the TB kernel.
-  TraceRange trace("heat.replay");
-  gpu::StencilGeom g;
-  g.pitch = L_.pitch;
-  g.gx0 = blk_.ox;
-  g.gy0 = blk_.oy;
-  g.nx = P_.nx;
-  g.ny = P_.ny;
-  g.cx = P_.cx;
-  g.cy = P_.cy;
-  g.numerics = int(P_.numerics);
-  const auto& nb = blk_.nbr;
-  for (int j = 0; j < rl; ++j) {
-    const int64_t e = rl - 1 - j;
-    const Box b{nb[North] >= 0 ? -e : 0, blk_.lx + (nb[South] >= 0 ? e : 0),
-                nb[West] >= 0 ? -e : 0, blk_.ly + (nb[East] >= 0 ? e : 0)};
-    gpu::lds_step(field_[cur], field_[cur ^ 1], g, b, nullptr, s_comp_);
-    cur ^= 1;
-  }
-  cur_ = cur;
-  gr_ = gc_ = 0;
-}
-
 void Solver::run_segments(int64_t steps, RunStats& s) {
   // Host-judged path (CPU backend, host-staged transports): one segment per
   // check, a host round trip per check.
@@ -940,10 +896,8 @@ void Solver::run_segments(int64_t steps, RunStats& s) {
 void Solver::run_gated(int64_t steps, RunStats& s) {
   // Device-judged path: segments of whole check periods are enqueued without
   // waiting on any check (two in flight; the host polls a pinned copy of the
-  // gate one segment behind).  Checks inside a pass are taken at their
-  // level; after the converging check every stencil launch is a no-op, so
-  // the state of that check is either a pass output or, for a check inside
-  // a pass, recomputed from the pass source (replay_steps).
+  // gate one segment behind).  After the converging check every stencil
+  // launch is a no-op, so the state of that check is its pass's output.
   const bool can_graph = P_.use_graph && !timing_ &&
                          (tr_->world() == 1 || tr_->graph_capturable()) &&
                          env_int("HEAT_GRAPH", 1) != 0;
@@ -998,17 +952,13 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
                           (long long)c));
   const PassRec* p = nullptr;
   for (const auto& r : all_recs)
-    if (r.step0 < c && c <= r.step0 + r.k) p = &r;
-  HEAT_CHECK(p != nullptr && p->rl == c - p->step0, "no pass holds check step %lld",
-             (long long)c);
-  if (p->rl == p->k) {
-    cur_ = p->cur1;
-    gr_ = p->gr1;
-    gc_ = p->gc1;
-  } else {
-    replay_steps(p->cur0, p->rl);
-    HIP_CHECK(hipStreamSynchronize(s_comp_));
-  }
+    if (r.step0 + r.k == c && r.rl == r.k) p = &r;
+  HEAT_CHECK(p != nullptr, "no pass ends at check step %lld", (long long)c);
+  // Passes behind the converging check wrote nothing: the state of that
+  // check is the output of its pass.
+  cur_ = p->cur1;
+  gr_ = p->gr1;
+  gc_ = p->gc1;
   step_ = c;
   s.steps_done = c - step0;
   s.converged = true;

@@ -163,7 +163,7 @@ _SIGS = {
                                   c_void_p, c_void_p]),
     "heat_op_tb_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                 c_float, c_float, POINTER(c_int64), c_int, c_int, c_void_p,
-                                c_void_p, c_int, c_int, c_int]),
+                                c_void_p, c_int, c_int]),
     "heat_tb_get_tuning": (c_int, [POINTER(HeatTbTuning)]),
     "heat_tb_set_tuning": (c_int, [POINTER(HeatTbTuning)]),
     "heat_op_tb_stamps": (c_int, [c_void_p, c_int64]),

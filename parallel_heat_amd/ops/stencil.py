@@ -42,7 +42,8 @@ class TbVariant(enum.IntFlag):
     SPLIT = 2048          # two-wave level-split pipelines (depths 8, 12)
     DIAG_CACHED_ROWS = 4096  # diagnostics: cache-resident input rows (wrong results)
     NO_AGE_PAIRS = 16384  # never age-group
-    LINEAR = 32768        # balanced plan: equal strip-rows per unit
+    LINEAR = 32768        # force the balanced plan: equal strip-rows per unit
+    NO_LINEAR = 65536     # never switch to it (default: when the classic plan fills < 90 %)
     DEFAULT = RAMP | SCALAR | XCD_GROUPS       # 23
     DEFAULT_DEEP = DEFAULT | SPLIT             # 2071
 
@@ -202,13 +203,11 @@ def mfma_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
 
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
-            waves_target: int = 0, variant: int = -1, res_level: int = 0) -> None:
+            waves_target: int = 0, variant: int = -1) -> None:
     """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes.
 
     variant: -1 = chosen per launch (TbVariant.DEFAULT, or DEFAULT_DEEP for
-    large depth-12 launches); otherwise TbVariant flags.  res_level: the
-    residual (resid given) is max|u_l - u_(l-1)| after step l = res_level of
-    the pass (0 = depth).
+    large depth-12 launches); otherwise TbVariant flags.
     """
     if src.device.type == "cpu":
         raise ValueError("tb_step is a GPU kernel")
@@ -222,7 +221,7 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
     _native.call("heat_op_tb_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
                  src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy, arr,
                  len(boxes), depth, ctypes.c_void_p(rp) if rp else None,
-                 ctypes.c_void_p(_stream()), waves_target, int(variant), int(res_level))
+                 ctypes.c_void_p(_stream()), waves_target, int(variant))
 
 
 def tb_stamps(buf: Optional[torch.Tensor]) -> None:

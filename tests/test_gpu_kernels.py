@@ -156,23 +156,55 @@ def test_tb_residual(gpu, k, variant):
     assert ops.resid_value(resid) == float((last - prev).abs().max())
 
 
-@pytest.mark.parametrize("k,variant,lx", [(12, DEEP, 700), (12, DEF, 203), (8, DEEP, 500),
-                                          (8, V.RING3, 203), (5, V.RAMP, 203),
-                                          (12, DEF | V.ALT_DIRECTION, 900)])
-def test_tb_residual_at_inner_level(gpu, k, variant, lx):
-    # A convergence check inside a pass: the residual after step l of the
-    # pass (both stages of the split pipeline, the ramp, the main loop and the
-    # mirrored chunks), the output unchanged.
-    ly = 517
-    g, a, b = _fields(lx, ly, k, gpu)
-    levels = [_cpu_steps(g, lx, ly, k, j) for j in range(k + 1)]
-    for lvl in sorted({1, 2, k // 2, k // 2 + 1, k - 1, k}):
+@pytest.mark.parametrize("variant", [DEF, DEEP, V.RING3, DEF | V.LINEAR, DEEP | V.LINEAR])
+def test_tb_residual_propagates_nan_and_inf(gpu, variant):
+    # The residual max is NaN-propagating: one non-finite cell reaches the
+    # judge (a NaN-dropping max would report the finite cells' maximum).
+    k, lx, ly = 8, 300, 517
+    for bad in (float("nan"), float("inf")):
+        g, a, b = _fields(lx, ly, k, gpu)
+        a.owned()[150, 200] = bad
+        b.owned()[150, 200] = bad
         resid = torch.zeros(1, dtype=torch.int32, device=gpu)
-        ops.tb_step(a, b, g, k, resid=resid, variant=variant, waves_target=512, res_level=lvl)
+        ops.tb_step(a, b, g, k, resid=resid, variant=variant)
         torch.cuda.synchronize()
-        want = float((levels[lvl] - levels[lvl - 1]).abs().max())
-        assert ops.resid_value(resid) == want, (lvl, ops.resid_value(resid), want)
-        assert torch.equal(b.owned().cpu(), levels[k])
+        r = ops.resid_value(resid)
+        assert not np.isfinite(r), (bad, r)
+
+
+@pytest.mark.parametrize("variant", [DEF | V.LINEAR, DEEP | V.LINEAR, RAMP_S | V.LINEAR,
+                                     DEF | V.LINEAR | V.ALT_DIRECTION])
+@pytest.mark.parametrize("lx,ly,waves", [(203, 517, 0), (203, 517, 7), (2600, 300, 0),
+                                         (1000, 2000, 96), (64, 3000, 333)])
+def test_tb_linear_plan_bitwise(gpu, variant, lx, ly, waves):
+    # Balanced linear plans: units crossing strip ends, segments split at
+    # the plate's masked edge rows, age pairs, mirrored segments, the LDS
+    # ring sequence carried across the segments of a split pipeline.
+    k = 12 if variant & V.SCALAR and not variant & V.FLOAT2 else 8
+    g, a, b = _fields(lx, ly, k, gpu)
+    resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.tb_step(a, b, g, k, resid=resid, waves_target=waves, variant=variant)
+    torch.cuda.synchronize()
+    prev = _cpu_steps(g, lx, ly, k, k - 1)
+    ref = _cpu_steps(g, lx, ly, k, k)
+    assert torch.equal(b.owned().cpu(), ref)
+    assert ops.resid_value(resid) == float((ref - prev).abs().max())
+
+
+def test_tb_linear_plan_interior_block(gpu):
+    # A block inside a larger plate (every segment unmasked), linear plan vs
+    # the full-plate oracle.
+    NX, NY, k = 400, 1200, 12
+    ox, oy, lx, ly = 100, 256, 180, 700
+    g = ops.Geom(nx=NX, ny=NY, gx0=ox, gy0=oy)
+    a = ops.Field(lx, ly, k, gpu)
+    b = ops.Field(lx, ly, k, gpu)
+    ops.init_field(a, g, "random", 5)
+    ops.init_field(b, g, "random", 5)
+    ops.tb_step(a, b, g, k, waves_target=50, variant=DEEP | V.LINEAR)
+    torch.cuda.synchronize()
+    full = _cpu_steps(ops.Geom(nx=NX, ny=NY), NX, NY, 1, k, seed=5)
+    assert torch.equal(b.owned().cpu(), full[ox:ox + lx, oy:oy + ly])
 
 
 @pytest.mark.parametrize("k,variant", [(8, DEF), (12, DEF), (8, DEEP), (12, DEEP)])

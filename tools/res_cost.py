@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Cost of the fused convergence residual in a TB pass: ms per pass without a
-residual, with the residual at the last level, and at inner levels (a check
-that falls inside the pass), per variant, interleaved rounds, median.
+"""Cost of a convergence check in TB passes: ms per pass with and without the
+fused residual, per variant and pass depth (interleaved rounds, median).  A
+check cuts its segment's passes (12,12,12,7,7 for 50 steps), so the depths of
+the cut passes matter as much as the residual itself.
 
-    python tools/res_cost.py --n 8192 --depth 12 --variants -1,23 --levels 0,12,8,6,4
+    python tools/res_cost.py --n 8192 --depths 12,8,7 --variants 2071,23
 """
 import argparse
 import json
@@ -11,6 +12,7 @@ import os
 import statistics
 import sys
 
+# HEAT_PY_ROOT: time another copy of the package (a previous build).
 sys.path.insert(0, os.environ.get("HEAT_PY_ROOT") or
                 os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -23,57 +25,53 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--nx", type=int, default=0)
-    ap.add_argument("--depth", type=int, default=12)
+    ap.add_argument("--depths", default="12,8,7")
     ap.add_argument("--variants", default="-1")
-    ap.add_argument("--levels", default="0,12,8,6,4", help="0 = no residual")
     ap.add_argument("--passes", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     nx = a.nx or a.n
-    k = a.depth
+    depths = [int(x) for x in a.depths.split(",")]
+    H = max(depths)
     g = ops.Geom(nx=nx, ny=a.n)
-    x = ops.Field(nx, a.n, k, dev)
-    y = ops.Field(nx, a.n, k, dev)
+    x = ops.Field(nx, a.n, H, dev)
+    y = ops.Field(nx, a.n, H, dev)
     ops.init_field(x, g, "random", 1)
     ops.init_field(y, g, "random", 1)
     resid = torch.zeros(4, dtype=torch.int32, device=dev)
-    combos = [(int(v), int(lv)) for v in a.variants.split(",") for lv in a.levels.split(",")]
-    has_level = "res_level" in ops.tb_step.__code__.co_varnames
+    combos = [(int(v), k, r) for v in a.variants.split(",") for k in depths for r in (False, True)]
 
-    def launch(v, lv, src, dst):
-        kw = {"variant": v}
-        if lv > 0:
-            kw["resid"] = resid
-            if has_level:
-                kw["res_level"] = lv
-            elif lv != k:
-                return False
-        ops.tb_step(src, dst, g, k, **kw)
-        return True
+    def launch(c, src, dst):
+        v, k, r = c
+        if k > 8 and k != 12:
+            return
+        ops.tb_step(src, dst, g, k, resid=resid if r else None,
+                    variant=v if (k == 12 or v < 0 or not v & 2048 or k == 8) else -1)
 
-    ok = {c: launch(c[0], c[1], x, y) for c in combos}
+    for c in combos:
+        launch(c, x, y)
     torch.cuda.synchronize()
-    res = {c: [] for c in combos if ok[c]}
+    res = {c: [] for c in combos}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
-        for c in res:
+        for c in combos:
             src, dst = x, y
             e0.record()
             for _ in range(a.passes):
-                launch(c[0], c[1], src, dst)
+                launch(c, src, dst)
                 src, dst = dst, src
             e1.record()
             e1.synchronize()
             res[c].append(e0.elapsed_time(e1) / a.passes)
-    base = {v: statistics.median(res[(v, 0)]) for v, lv in res if lv == 0 and (v, 0) in res}
     for c, t in res.items():
+        v, k, r = c
         med = statistics.median(t)
-        row = {"variant": c[0], "res_level": c[1], "ms_per_pass": round(med, 4),
-               "tcells_s": round(nx * a.n * k / (med * 1e-3) / 1e12, 3)}
-        if c[0] in base:
-            row["vs_no_resid"] = round(med / base[c[0]], 4)
-        print(json.dumps(row))
+        base = statistics.median(res[(v, k, False)])
+        print(json.dumps({"variant": v, "depth": k, "resid": r, "ms_per_pass": round(med, 4),
+                          "ms_per_step": round(med / k, 5),
+                          "tcells_s": round(nx * a.n * k / (med * 1e-3) / 1e12, 3),
+                          "vs_no_resid": round(med / base, 4)}))
 
 
 if __name__ == "__main__":
