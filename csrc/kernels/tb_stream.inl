@@ -685,13 +685,34 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       x0 = y0;
     }
   }
-  // One call site of the (large, inlined) segment body: classic plans run
-  // one segment, linear plans as many as their range crosses.
-  int64_t qoff = 0;
-  while (x0 < x1) {
+  if (!linear) {
+    // Classic plan: one (strip, chunk) segment, called directly (a loop
+    // around the inlined segment body measured ~3 % slower at 8192^2).
     int bi = 0;
-    int64_t rb, re;
-    if (linear) {
+#pragma unroll
+    for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
+      if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
+    const TbBox& bx = a.box[bi];
+    const int w = wave - bx.wave_begin;
+    strip = w % bx.nstrips;
+    chunk = w / bx.nstrips;
+    int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
+    int64_t re = min(rb + bx.chunk_len, bx.r1);
+    if (pairs) {
+      // Box chunks are groups of G * chunk_len rows; age a takes rows
+      // [age_cum[a], age_cum[a+1]) / 1024 of its group.
+      const int G = a.age_groups;
+      const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
+      const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
+      rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
+      re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
+    }
+    if (rb < re) m = tb_segment<K, LAG, K1>(a, bx, strip, chunk, rb, re, stage, ring, cnt, 0);
+  } else {
+    // Linear plan: as many segments as the unit's range crosses.
+    int64_t qoff = 0;
+    while (x0 < x1) {
+      int bi = 0;
 #pragma unroll
       for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
         if (j < a.nbox && x0 >= a.box[j].lin0) bi = j;
@@ -699,39 +720,18 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       const int64_t rows = bx.r1 - bx.r0;
       const int64_t off = x0 - bx.lin0;
       strip = int(off / rows);
-      rb = bx.r0 + off % rows;
-      re = min(bx.r1, rb + (x1 - x0));
+      const int64_t rb = bx.r0 + off % rows;
+      int64_t re = min(bx.r1, rb + (x1 - x0));
       // Rows whose K-window reaches the plate's top / bottom row run the
       // masked (generic) path: keep them in segments of their own.
       const int64_t top = 1 - a.g.gx0 + K, bot = a.g.nx - 1 - a.g.gx0 - K;
       if (rb < top && re > top) re = top;
       else if (rb < bot && re > bot) re = bot;
       x0 += re - rb;
-    } else {
-#pragma unroll
-      for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
-        if (j < a.nbox && wave >= a.box[j].wave_begin) bi = j;
-      const TbBox& bx = a.box[bi];
-      const int w = wave - bx.wave_begin;
-      strip = w % bx.nstrips;
-      chunk = w / bx.nstrips;
-      rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
-      re = min(rb + bx.chunk_len, bx.r1);
-      if (pairs) {
-        // Box chunks are groups of G * chunk_len rows; age a takes rows
-        // [age_cum[a], age_cum[a+1]) / 1024 of its group.
-        const int G = a.age_groups;
-        const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
-        const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
-        rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
-        re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
-      }
-      x0 = x1;  // one segment
-      if (rb >= re) break;
+      m = __builtin_elementwise_maximum(
+          m, tb_segment<K, LAG, K1>(a, bx, strip, chunk, rb, re, stage, ring, cnt, qoff));
+      qoff += (re - rb) + 2 * K2;
     }
-    m = __builtin_elementwise_maximum(
-        m, tb_segment<K, LAG, K1>(a, a.box[bi], strip, chunk, rb, re, stage, ring, cnt, qoff));
-    qoff += (re - rb) + 2 * K2;
   }
   if (a.resid != nullptr && (K1 == 0 || stage == 1)) wave_max_atomic(__float_as_uint(m), a.resid);
   if (a.stamps && lane == 0) {
@@ -905,7 +905,10 @@ int occ_split_k() {
   }
   return std::max(1, n);
 }
-// Level-split launches: depth 8 (4 + 4) and 12 (6 + 6).
+// Level-split launches: depth 8 (4 + 4) and 12 (6 + 6).  14 (7 + 7) and
+// 16 (8 + 8) were built for an A/B and removed: 3.73 / 3.85 vs 5.02
+// Tcells/s at 8192^2, bench 3.83 / 3.80 vs 5.17 (3 waves per SIMD,
+// profiles/r3_raw/r3ab3_*.log).
 bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
   switch (depth) {
     case 8: launch_split_k<8, 4>(args, st); return true;
