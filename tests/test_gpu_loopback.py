@@ -174,3 +174,25 @@ def test_loopback_failed_rank_unblocks_peers(gpu):
 
     with pytest.raises(RuntimeError, match="rank 1 failed: injected failure"):
         run_group(cfg, 2, fn)
+
+
+@pytest.mark.parametrize("world,kw", [(2, dict(decomp="rows", tb_depth=12)),
+                                      (4, dict(decomp="auto", tb_depth=8))])
+def test_loopback_vs_torch_fp32(gpu, world, kw):
+    # The direct PyTorch anchor for the multi-rank path: a decomposed
+    # deep-halo TB run against K applications of the plain fp32 stencil
+    # (R.step_torch) on the GPU, tolerance growing with K.
+    import torch
+    steps = 60
+    cfg = HeatConfig(**{**BASE, "nx": 300, "ny": 280, **kw})
+
+    def fn(s):
+        s.run(steps)
+        return s.gather()
+
+    got = next(g for g in run_group(cfg, world, fn) if g is not None)
+    u = torch.from_numpy(R.init_grid(300, 280, "random", BASE["seed"])).cuda()
+    for _ in range(steps):
+        u = R.step_torch(u)
+    torch.testing.assert_close(torch.from_numpy(got), u.cpu(), rtol=2e-6 * steps,
+                               atol=1e-5 * steps)
