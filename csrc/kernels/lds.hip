@@ -55,11 +55,18 @@ __device__ __forceinline__ float lds_update(float c, float n, float s, float w, 
 template <int NUMERICS>
 __global__ __launch_bounds__(256) void lds_kernel(const float* __restrict__ src,
                                                   float* __restrict__ dst, StencilGeom g, Box box,
-                                                  int64_t c_base, unsigned* resid) {
+                                                  int64_t c_base, int ntx, int nty,
+                                                  unsigned* resid) {
   __shared__ float4 tile[(kLdsRows + 2) * kLdsPitch4];
   if (tbdetail::gated(g.gate)) return;  // uniform: before the barrier
-  const int64_t r0 = box.r0 + int64_t(blockIdx.y) * kLdsRows;
-  const int64_t cb = c_base + int64_t(blockIdx.x) * kLdsCols;  // multiple of 4
+  // XCD-aware tile order (blocks b, b+8, ... share an XCD): each XCD takes a
+  // contiguous row-major range of tiles, so the halo lines of neighbouring
+  // tiles are fetched once per XCD L2 instead of once per tile.
+  const int nt = ntx * nty, b = blockIdx.x, x8 = b & 7, j = b >> 3;
+  const int q = nt >> 3, rem = nt & 7;
+  const int t = x8 * q + min(x8, rem) + j;
+  const int64_t r0 = box.r0 + int64_t(t / ntx) * kLdsRows;
+  const int64_t cb = c_base + int64_t(t % ntx) * kLdsCols;  // multiple of 4
   // Cooperative staging of rows r0-1 .. r0+kLdsRows and float4 columns
   // cb-4 .. cb+kLdsCols+3.  Loads are clamped to the cells the box's
   // stencil can touch (rows [r0box-1, r1box], columns [c0-1, c1]), which
@@ -127,11 +134,14 @@ void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box
   if (box.empty()) return;
   // Tiles start on a float4 column (origin and pitch are 16-byte aligned).
   const int64_t c_base = floor4(box.c0);
-  dim3 grid(unsigned(ceil_div(box.c1 - c_base, kLdsCols)), unsigned(ceil_div(box.rows(), kLdsRows)));
+  const int ntx = int(ceil_div(box.c1 - c_base, kLdsCols)), nty = int(ceil_div(box.rows(), kLdsRows));
+  const dim3 grid(unsigned(ntx) * unsigned(nty));
   if (g.numerics == 1)
-    hipLaunchKernelGGL(lds_kernel<1>, grid, dim3(256), 0, st, src, dst, g, box, c_base, resid);
+    hipLaunchKernelGGL(lds_kernel<1>, grid, dim3(256), 0, st, src, dst, g, box, c_base, ntx, nty,
+                       resid);
   else
-    hipLaunchKernelGGL(lds_kernel<0>, grid, dim3(256), 0, st, src, dst, g, box, c_base, resid);
+    hipLaunchKernelGGL(lds_kernel<0>, grid, dim3(256), 0, st, src, dst, g, box, c_base, ntx, nty,
+                       resid);
   HIP_CHECK(hipGetLastError());
 }
 

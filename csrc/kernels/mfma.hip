@@ -50,11 +50,18 @@ __host__ __device__ inline int64_t floor4(int64_t x) { return x & ~int64_t(3); }
 
 __global__ __launch_bounds__(256) void mfma_kernel(const float* __restrict__ src,
                                                    float* __restrict__ dst, StencilGeom g, Box box,
-                                                   int64_t c_base, unsigned* resid) {
+                                                   int64_t c_base, int ntx, int nty,
+                                                   unsigned* resid) {
   __shared__ float tile[(kTileRows + kPadRows) * kPitch];
   if (tbdetail::gated(g.gate)) return;  // uniform: before the barrier
-  const int64_t R0 = box.r0 + int64_t(blockIdx.y) * kRows;
-  const int64_t cb = c_base + int64_t(blockIdx.x) * kCols;  // multiple of 4
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD (round-robin
+  // dispatch, observed), so each XCD takes a contiguous row-major range of
+  // tiles and the halo lines of side-by-side tiles hit its L2.
+  const int nt = ntx * nty, b = blockIdx.x, x8 = b & 7, j = b >> 3;
+  const int q = nt >> 3, r = nt & 7;
+  const int t = x8 * q + min(x8, r) + j;
+  const int64_t R0 = box.r0 + int64_t(t / ntx) * kRows;
+  const int64_t cb = c_base + int64_t(t % ntx) * kCols;  // multiple of 4
   // Stage rows R0-1 .. R0+64 and columns cb-4 .. cb+131: coalesced float4
   // loads, clamped to the cells the box's stencil can touch (rows
   // [r0-1, r1], columns [c0-1, c1]); clamped values are never used.
@@ -129,8 +136,9 @@ void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& bo
                unsigned* resid, hipStream_t st) {
   if (box.empty()) return;
   const int64_t c_base = floor4(box.c0);
-  dim3 grid(unsigned(ceil_div(box.c1 - c_base, kCols)), unsigned(ceil_div(box.rows(), kRows)));
-  hipLaunchKernelGGL(mfma_kernel, grid, dim3(256), 0, st, src, dst, g, box, c_base, resid);
+  const int ntx = int(ceil_div(box.c1 - c_base, kCols)), nty = int(ceil_div(box.rows(), kRows));
+  hipLaunchKernelGGL(mfma_kernel, dim3(unsigned(ntx) * unsigned(nty)), dim3(256), 0, st, src, dst,
+                     g, box, c_base, ntx, nty, resid);
   HIP_CHECK(hipGetLastError());
 }
 
