@@ -80,6 +80,12 @@ def rccl_links(path: str) -> list:
 
 
 def main() -> int:
+    # The JSON line is the only thing on stdout: native libraries (RCCL's
+    # version banner under NCCL_DEBUG=VERSION, ...) print there too, so fd 1
+    # is pointed at stderr and the JSON goes to a saved copy of it.
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -149,7 +155,7 @@ def main() -> int:
     rccl_log = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if "NCCL_DEBUG" not in os.environ:
+        if os.environ.get("NCCL_DEBUG", "").upper() not in ("INFO", "TRACE"):
             # Record which transport RCCL picks for each neighbour pair (xGMI
             # P2P on a node) in a per-rank file, reported in the JSON line.
             rccl_log = os.path.join(tempfile.gettempdir(),
@@ -284,7 +290,7 @@ def main() -> int:
                 "ranks": [{k: r[k] for k in ("rank", "user_rank", "device", "bus_id")}
                           for r in every],
                 "distinct_devices": len({r["bus_id"] or r["device"] for r in every}),
-                "links": links if rccl_log else "not recorded (NCCL_DEBUG set by the caller)"}
+                "links": links if rccl_log else "not recorded (NCCL_DEBUG=INFO/TRACE set by the caller)"}
     faulthandler.cancel_dump_traceback_later()
 
     cells = args.nx * args.ny * done
@@ -332,7 +338,7 @@ def main() -> int:
             line["phase_seconds_rank0"] = {"exchange": round(phases[0], 6),
                                            "compute": round(phases[1], 6),
                                            "reduce": round(phases[2], 6)}
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     solver.close()
     if shared is not None:
         shared.close()
