@@ -76,6 +76,9 @@ constexpr double kTbAgeRatio = 1.0;
 // grid takes 1.7x the rows of the second half in each pair of adjacent
 // chunks: +4-7 % at 2048..8192-row blocks (profiles/tb_split_age_pairs_r2.md).
 constexpr double kTbSplitAgeWeights[2] = {1.7, 1.0};
+// Linear plans of split pipelines at four blocks per CU: one share per
+// dispatch round (oldest first).
+constexpr double kTbLinearAgeWeights[4] = {2.0, 1.95, 1.15, 1.0};
 constexpr int kTbDeepDepth = 12;  // + 12: scalar ring-3+ramp build (variant bits 4|3)
 bool tb_depth_supported(int k);
 // Output columns per 256-column strip at depth k.

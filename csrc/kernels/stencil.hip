@@ -469,6 +469,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       weights.assign(2, 1.0);
     }
   }
+  int bpc = 0;  // blocks per CU of the planned launch (0: set by the caller's waves_target)
   if (waves_target <= 0) {
     // Whole rounds of the resident wave capacity (a partial last round leaves
     // SIMDs idle for the tail of the launch); by default with the number of
@@ -485,6 +486,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       // Blocks per CU = dispatch rounds: single-wave pipelines put one wave
       // per SIMD in a block, level-split blocks hold two pipelines (4 waves).
       const int blocks_per_cu = split_v ? 2 * per_simd : per_simd;
+      bpc = blocks_per_cu;
       if (G == 0 && blocks_per_cu >= 2 && !(variant & tbv::kFloat2) &&
           !(variant & tbv::kNoAgePairs))
         set_weights(blocks_per_cu);
@@ -613,6 +615,14 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       total += int64_t(t.nstrips) * B.rows();
     }
     if (n == 0) return;
+    // Long linear units accumulate the SIMD's age bias: with four blocks
+    // per CU every dispatch round gets its own row share
+    // (kTbLinearAgeWeights; 16384 x 131072 slab 4.70 -> 5.15 Tcells/s,
+    // profiles/r3_raw/r3age_a16384.log).
+    if (pairs && env_weights.empty() && split_v && bpc >= 4) {
+      weights.assign(std::begin(kTbLinearAgeWeights), std::end(kTbLinearAgeWeights));
+      G = int(weights.size());
+    }
     const int Gl = pairs ? G : 1;
     const int64_t units = std::max<int64_t>(
         Gl, std::min<int64_t>(waves_target, total / std::max<int64_t>(1, min_len)));
