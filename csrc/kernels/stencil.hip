@@ -21,10 +21,12 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <iterator>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -302,6 +304,25 @@ void tb_set_tuning(const TbTuning& t) {
 }
 
 int tb_default_rounds() { return tb_tuning().rounds; }
+
+namespace {
+bool tb_trace_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT_TB_TRACE");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+void tb_trace_once(const char* line) {
+  static std::mutex mu;
+  static std::vector<std::string> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const auto& s : seen)
+    if (s == line) return;
+  seen.emplace_back(line);
+  std::fputs(line, stderr);
+}
+}  // namespace
 
 int tb_simd_count() {
   static std::map<int, int> cache;
@@ -650,6 +671,18 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     }
   }
   const bool split = tb_variant_split(variant);
+  if (tb_trace_enabled()) {
+    // HEAT_TB_TRACE=1: each distinct plan once on stderr (planner checks).
+    char line[320];
+    std::snprintf(line, sizeof line,
+                  "[heat tb] depth %d variant %d boxes %d strip_rows %lld waves_target %d bpc %d "
+                  "linear %d units %d age_groups %d cum %d,%d,%d,%d chunk0 %d nchunks0 %d\n",
+                  depth, variant, n, (long long)total_strip_rows, waves_target, bpc,
+                  int((args.flags & tbdetail::kTbLinear) != 0), waves, pairs ? G : 0,
+                  args.age_cum[1], args.age_cum[2], args.age_cum[3], args.age_cum[4],
+                  args.box[0].chunk_len, args.box[0].nchunks);
+    tb_trace_once(line);
+  }
   if (const Stamps sb = stamps_of_current_device(); sb.buf) {
     const int64_t need = int64_t(waves) * (split ? 2 : 1);
     HEAT_CHECK(need <= sb.waves, "stamp buffer holds %lld waves, launch has %lld",

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--interior", action="store_true", help="block inside a larger plate")
     ap.add_argument("--launches", type=int, default=4)
+    ap.add_argument("--passes", type=int, default=40,
+                    help="back-to-back launches timed with events: wall per pass vs one launch's span")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = ops.Geom(nx=a.nx, ny=a.ny) if not a.interior else \
@@ -37,6 +39,14 @@ def main():
     for _ in range(a.launches):  # warm
         ops.tb_step(x, y, g, a.depth, waves_target=a.waves, variant=a.variant)
         x, y = y, x
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.passes):
+        ops.tb_step(x, y, g, a.depth, waves_target=a.waves, variant=a.variant)
+        x, y = y, x
+    e1.record()
+    e1.synchronize()
+    wall_us = e0.elapsed_time(e1) * 1e3 / max(1, a.passes)
     ops.tb_stamps(st)
     ops.tb_step(x, y, g, a.depth, waves_target=a.waves, variant=a.variant)
     torch.cuda.synchronize()
@@ -69,6 +79,9 @@ def main():
     nstr, nch = int(strip.max()) + 1, int(chunk.max()) + 1
     out = {
         "nx": a.nx, "ny": a.ny, "depth": a.depth, "waves": int(s.shape[0]), "span_us": round(span, 1),
+        "wall_per_pass_us": round(wall_us, 1),
+        "gap_us": round(wall_us - span, 1),
+        "gcells_s_wall": round(a.nx * a.ny * a.depth / wall_us * 1e-3, 1),
         "mean_dur_us": round(float(dur.mean()), 1), "min_dur_us": round(float(dur.min()), 1),
         "max_dur_us": round(float(dur.max()), 1), "busy_fraction": round(float(dur.sum()) / (span * s.shape[0]), 3),
         "start_max_us": round(float(start.max()), 1),
@@ -117,6 +130,12 @@ def main():
     last.index_reduce_(0, slot, end, "amax", include_self=False)
     used = last[torch.unique(slot)]
     out["simd_last_end_p10_p50_p90_us"] = [round(float(used.quantile(q)), 1) for q in (0.1, 0.5, 0.9)]
+    # Row redundancy of the plan (classic plans: every chunk streams its rows
+    # plus the K-1 rows of the trapezoid on each side, averaged over levels)
+    # and the column redundancy of a 256-column strip with a K-column halo.
+    ch = a.nx / nch
+    out["row_redundancy"] = round((ch + a.depth - 1) / ch, 3)
+    out["col_redundancy"] = round(a.ny and (256 * nstr) / a.ny, 3)
     print(json.dumps(out))
 
 
