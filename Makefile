@@ -32,7 +32,7 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp
 	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -x hip -c $< -o $@
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
-$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)
@@ -57,7 +57,7 @@ ASM ?= tb_split
 asm:
 	@mkdir -p $(BUILD)/asm
 	cd $(BUILD)/asm && $(HIPCC) $(patsubst -Icsrc/include,-I../../csrc/include,$(HIPFLAGS)) \
-	  $(if $(filter tb_scalar tb_split,$(ASM)),-fno-slp-vectorize) --offload-device-only -S \
+	  $(if $(filter tb_scalar tb_split tb_tile,$(ASM)),-fno-slp-vectorize) --offload-device-only -S \
 	  -o $(ASM).s ../../csrc/kernels/$(ASM).hip
 
 resources: $(SRCS_HIP)

@@ -160,12 +160,15 @@ int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, in
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,
                     int variant /* -1 default; heat::gpu::tbv flags */);
-/* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares. */
+/* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares;
+   tile_rows / tile_waves: rows per wave / waves per workgroup of tile launches
+   (0 = planner). */
 typedef struct heat_tb_tuning {
   int32_t variant, rounds, min_len, waves;
   double edge_frac;
-  int32_t n_weights, pad_;
+  int32_t n_weights, tile_rows;
   double weights[4];
+  int32_t tile_waves, pad_;
 } heat_tb_tuning;
 int heat_tb_get_tuning(heat_tb_tuning* out);
 int heat_tb_set_tuning(const heat_tb_tuning* in);

@@ -58,6 +58,9 @@ enum : int {
   kLinear = 32768,      // force the balanced linear plan (equal strip-rows per unit)
   kNoLinear = 65536,    // never switch to it (by default it replaces a classic
                         // plan that fills < 90 % of the launch's units)
+  kTile = 131072,       // workgroup tiles: 8 waves x R rows of a strip in VGPRs,
+                        // neighbour rows through LDS each step (tbw, tb_tile.hip)
+  kTileDpp = 262144,    // with kTile: DPP lane shifts instead of ds_bpermute
   // Defaults: depth <= 8 and small launches at 12; large launches at 12.
   kDefault = kRamp | kScalar | kXcdGroups,  // 23
   kDefaultDeep = kDefault | kSplit,         // 2071
@@ -149,6 +152,8 @@ struct TbTuning {
   // HEAT_TB_AGE_WEIGHTS "w0,w1,.." (or HEAT_TB_AGE_RATIO r = {r, 1}): row
   // shares of the age groups; empty = the built-in weights.
   std::vector<double> age_weights;
+  int tile_rows = 0;       // HEAT_TB_TILE_ROWS: rows per wave of kTile launches (0: planner)
+  int tile_waves = 0;      // HEAT_TB_TILE_WAVES: waves per kTile workgroup, 8 or 16 (0: planner)
 };
 TbTuning tb_tuning();  // a copy of the current set
 void tb_set_tuning(const TbTuning& t);

@@ -34,6 +34,7 @@
 #include "heat/init_fn.hpp"
 #include "heat/kernels.hpp"
 #include "tb_common.hpp"
+#include "tb_tile.hpp"
 
 namespace heat::gpu {
 namespace {
@@ -272,6 +273,8 @@ TbTuning tuning_from_env() {
   t.rounds = std::max(0, geti("HEAT_TB_ROUNDS", 0));
   t.min_len = std::max(0, geti("HEAT_TB_MINLEN", 0));
   t.waves = std::max(0, geti("HEAT_TB_WAVES", 0));
+  t.tile_rows = std::max(0, geti("HEAT_TB_TILE_ROWS", 0));
+  t.tile_waves = std::max(0, geti("HEAT_TB_TILE_WAVES", 0));
   if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);
   if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
     for (const char* q = e; *q;) {
@@ -393,6 +396,10 @@ int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
   // 8192, 2048 x 4096, 1536 x 8192, ...) one wave per (strip, chunk) at
   // depth 12 is 8-12 % faster, above it the split is 2-4 % faster
   // (profiles/tb_block_shapes_r2.md).
+  // Below ~48 (the 8-GPU blocks 1024 x 8192 and 2048 x 4096 and their
+  // deep-halo passes) the workgroup tiles win: +6-7 % over one wave per
+  // chunk; at 54 they lose 8 % (profiles/r3_tile.md).
+  if (depth == kTbDeepDepth && strip_rows_per_simd < 48) return tbv::kTile | tbv::kXcdGroups;
   if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
   return tb_default_variant(depth);
 }
@@ -453,6 +460,15 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     for (int b = 0; b < nbox; ++b)
       if (!boxes[b].empty()) rows4 += ceil_div(boxes[b].cols(), W4) * boxes[b].rows();
     variant = tb_auto_variant(depth, rows4 / tb_simd_count());
+  }
+  if (variant & tbv::kTile) {
+    // The tile kernel runs steps in (down, up) pairs: even depths only; an
+    // odd pass (a remainder or a check-cut pass) streams.
+    if (depth % 2 == 0) {
+      tbw::step(src, dst, g, boxes, nbox, depth, resid, st, variant, tune);
+      return;
+    }
+    variant &= ~(tbv::kTile | tbv::kTileDpp);
   }
   const int lag = tb_variant_lag(variant);
   const int W = tb_strip_width(depth, tb_lane_cols(variant));

@@ -1,0 +1,477 @@
+// Workgroup-tile temporally blocked Jacobi kernel (variant bit kTile).
+//
+// The register-streaming kernel (tb_stream.inl) gives every wave its own
+// (strip, chunk) and pays the trapezoid of classic temporal blocking: each
+// chunk recomputes K - l rows beyond both of its ends at level l.  On the
+// per-rank blocks of 4-8 GPU runs (1024 x 8192, 2048 x 4096: 36 strip-rows per
+// SIMD) that is 1.30x the useful row updates, and there is only room for one
+// wave per SIMD, which issues a VALU op every ~4-6 cycles instead of ~2-3
+// (profiles/r3_small_blocks.md).
+//
+// Here a workgroup of NW = 8 (or 16) waves owns one tile: a 256-column strip (64 lanes
+// x float4) by NW * R rows, every wave R consecutive rows held in VGPRs for
+// the whole launch.  A time step updates all rows in place; the only data a
+// wave needs from outside its registers are the last row of the wave above
+// and the first row of the wave below, exchanged through LDS (one barrier per
+// step, double-buffered slots).  So the tile pays only its own K-deep ghost
+// ring (2K of NW * R rows, round_up(K, 4) columns per side) instead of a
+// trapezoid per wave, and runs two (R >= 20) or four (R <= 16) waves per SIMD.
+// East/west neighbours cross lanes with ds_bpermute (BP) or DPP wave shifts.
+//
+// Input rows [r0 - K, r1 + K) and columns [c0 - round_up(K, 4), ...) of each
+// box are read (the same footprint as tb_stream.inl); rows of the tile past
+// that range load a clamped (valid, don't-care) row: their values only reach
+// rows outside the useful range within K steps.  The update is heat::stencil,
+// so results are bitwise identical to every other kernel.
+//
+// Reference kernel this replaces: cuda/cuda_heat.cu:140-163 (one step per
+// launch, global memory) and :42-138 (the fused residual).
+#include "tb_tile.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <tuple>
+#include <type_traits>
+
+#include "heat/common.hpp"
+
+namespace heat::gpu::tbw {
+
+using tbdetail::TbArgs;
+using tbdetail::TbBox;
+typedef float vecf __attribute__((ext_vector_type(4)));
+
+#ifndef HEAT_TILE_PD
+#define HEAT_TILE_PD 3  // rows the ds_bpermute lane shifts run ahead
+#endif
+
+// Lane l <- lane l-1 / l+1.  Lanes 0 and 63 lie in the strip overlap
+// (don't-care values).
+template <bool BP>
+__device__ __forceinline__ float from_left(float v) {
+  if constexpr (BP) {
+    const int l = threadIdx.x & 63;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 63) & 63) << 2, __float_as_int(v)));
+  } else {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+  }
+}
+template <bool BP>
+__device__ __forceinline__ float from_right(float v) {
+  if constexpr (BP) {
+    const int l = threadIdx.x & 63;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 1) & 63) << 2, __float_as_int(v)));
+  } else {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+  }
+}
+
+// cx / cy in VGPRs: a VALU op with an SGPR operand issues at half rate.
+__device__ __forceinline__ float to_vgpr(float x) {
+  float r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
+// A wave-uniform value the compiler must treat as unknown from here on.
+// (readfirstlane: values read from the kernel arguments through a dynamic box
+// index are not provably uniform to the compiler.)
+__device__ __forceinline__ void opaque(unsigned& x) {
+  x = __builtin_amdgcn_readfirstlane(x);
+  asm volatile("" : "+s"(x));
+}
+__device__ __forceinline__ void opaque(int64_t& x) {
+  unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(uint64_t(x)));
+  unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(uint64_t(x) >> 32));
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  x = int64_t((uint64_t(hi) << 32) | lo);
+}
+
+// LDS writes of this wave done, then the workgroup barrier.  Not
+// __syncthreads(): its fence would also wait for the wave's outstanding
+// global loads (the tile's rows still streaming in at step 0) and stores.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// MODE 0: no cell of the tile is on the plate's fixed ring (or outside it);
+// MODE 1: per-lane column masks and a per-row (uniform) mask keep those cells.
+template <int MODE, bool BP>
+struct Upd {
+  float cx, cy;
+  bool cm[4];
+  // wl / er: the west neighbour of element 0 (lane l-1's element 3) and the
+  // east neighbour of element 3 (lane l+1's element 0).
+  __device__ __forceinline__ vecf apply(const vecf& a, const vecf& b, const vecf& c, float wl,
+                                        float er, bool row_ok) const {
+    vecf r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = j == 0 ? wl : b[j - 1];
+      const float e = j == 3 ? er : b[j + 1];
+      // The shifted value as the second operand of e + w (fp add commutes):
+      // the DPP build folds it into v_add_f32_dpp.
+      r[j] = j == 3 ? stencil(b[j], a[j], c[j], e, w, cx, cy) : stencil(b[j], a[j], c[j], w, e, cx, cy);
+    }
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = (cm[j] && row_ok) ? r[j] : b[j];
+    }
+    return r;
+  }
+};
+
+template <int R, int MODE, bool RES, bool BP>
+struct Tile {
+  vecf u[R];
+  float m = 0.f;
+
+  // One time step of this wave's rows, in place, top-down (DOWN) or
+  // bottom-up.  above / below: the last row of the wave above and the first
+  // row of the wave below (old values).  Alternating the direction every step
+  // lets the register allocator put new row r where old row r -/+ 1 was (dead
+  // by then) and be back at the loop's assignment after two steps: one
+  // direction only needed a copy of every row per step at the back-edge.
+  // LAST: the launch's last step stores every useful row as soon as it is
+  // computed (dst + off0 + r * pitch, this lane's columns if store_lane) and,
+  // with RES, accumulates max |new - old| over the useful cells.
+  template <bool DOWN, bool LAST>
+  __device__ __forceinline__ void step(const vecf& above, const vecf& below, const Upd<MODE, BP>& up,
+                                       unsigned rowmask, unsigned usemask, bool store_lane, int rc,
+                                       float* __restrict__ dst, int64_t off0, int64_t pitch) {
+    // Lane shifts of the OLD rows.  ds_bpermute results take ~50+ cycles: the
+    // shifts of the row PD places ahead in processing order are issued before
+    // a row is computed (scheduling barriers keep that order; unconstrained,
+    // the scheduler hoisted every row's shifts and spilled).  DPP shifts fold
+    // into the add.
+    constexpr int PD = BP ? (R - 1 < HEAT_TILE_PD ? R - 1 : HEAT_TILE_PD) : 0;
+    float wl[R], er[R];
+    auto row_at = [](int i) { return DOWN ? i : R - 1 - i; };
+    auto shift = [&](int r) {
+      wl[r] = from_left<BP>(u[r][3]);
+      er[r] = from_right<BP>(u[r][0]);
+    };
+    if constexpr (BP) {
+#pragma unroll
+      for (int i = 0; i < PD; ++i) shift(row_at(i));
+    }
+    vecf prev = u[row_at(0)];  // old value of the row processed before
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int r = row_at(i);
+      if (i + PD < R) shift(row_at(i + PD));
+      const vecf cur = u[r];
+      const vecf n = r == 0 ? above : (DOWN ? prev : u[r - 1]);
+      const vecf so = r == R - 1 ? below : (DOWN ? u[r + 1] : prev);
+      u[r] = up.apply(n, cur, so, wl[r], er[r], (rowmask >> r) & 1u);
+      if constexpr (LAST) {
+        if ((usemask >> r) & 1u) {
+          if (store_lane) *reinterpret_cast<vecf*>(dst + off0 + r * pitch) = u[r];
+          if constexpr (RES) acc(u[r], cur, store_lane, rc);
+        }
+      }
+      prev = cur;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  __device__ __forceinline__ void acc(const vecf& nw, const vecf& old, bool res_lane, int rc) {
+    // NaN-propagating max (v_maximum3_f32): a NaN or inf reaches the judge.
+    if (res_lane) {
+      float d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = (j == 0 || rc > j) ? __builtin_fabsf(nw[j] - old[j]) : 0.f;
+      m = __builtin_elementwise_maximum(
+          m, __builtin_elementwise_maximum(__builtin_elementwise_maximum(d[0], d[1]),
+                                           __builtin_elementwise_maximum(d[2], d[3])));
+    }
+  }
+};
+
+template <int R, int NW, int MODE, bool RES, bool BP>
+__device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int strip, int t, int K,
+                                          vecf (*xch)[2][NW][64]) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const StencilGeom& g = a.g;
+  const int KK = (K + 3) & ~3;
+  const int64_t Wd = 256 - 2 * KK;
+  const int64_t cbase = bx.c0 + int64_t(strip) * Wd;
+  const int64_t cend = min(cbase + Wd, bx.c1);
+  const int64_t col = cbase - KK + 4 * lane;
+  const bool store_lane = col >= cbase && col < cend;
+  const int rc = int(min<int64_t>(cend - col, 4));
+  const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;  // useful rows [ub, ue)
+  const int64_t ue = min(ub + bx.chunk_len, bx.r1);
+  const int64_t row0 = ub - K + int64_t(w) * R;         // this wave's first row
+  const int64_t rmin = bx.r0 - K, rmax = bx.r1 + K - 1;  // readable rows
+  const int64_t pitch = g.pitch;
+  const float* __restrict__ src = a.src + (cbase - KK);  // wave-uniform; + 4*lane
+  float* __restrict__ dst = a.dst + (cbase - KK);
+  const int lo = 4 * lane;
+
+  Tile<R, MODE, RES, BP> T;
+  // Row offsets are made opaque (asm) so the compiler neither keeps R 64-bit
+  // row offsets alive from the loads to the stores (CSE) nor hoists per-row
+  // masks out of the step loop: both spilled SGPRs into VGPR lanes.
+  auto ld = [&](int r) {
+    int64_t row = min(max(row0 + r, rmin), rmax);
+    opaque(row);
+    return *reinterpret_cast<const vecf*>(src + row * pitch + lo);
+  };
+  // The first and last rows go to LDS at step 0: load them first.
+  T.u[0] = ld(0);
+  T.u[R - 1] = ld(R - 1);
+#pragma unroll
+  for (int r = 1; r < R - 1; ++r) T.u[r] = ld(r);
+
+  Upd<MODE, BP> up;
+  up.cx = to_vgpr(g.cx);
+  up.cy = to_vgpr(g.cy);
+  // Bit r: row row0 + r is a global interior row (MODE 1) / a useful row.
+  auto bits = [](int64_t lo_r, int64_t hi_r) -> unsigned {  // rows [lo_r, hi_r) of 0..R-1
+    const int l = int(max<int64_t>(0, min<int64_t>(lo_r, R)));
+    const int h = int(max<int64_t>(0, min<int64_t>(hi_r, R)));
+    const unsigned top = h >= 32 ? ~0u : (1u << h) - 1u;
+    return l >= h ? 0u : top & ~((1u << l) - 1u);
+  };
+  unsigned rowmask = MODE == 1 ? bits(1 - (g.gx0 + row0), g.nx - 1 - (g.gx0 + row0)) : ~0u;
+  unsigned usemask = bits(ub - row0, ue - row0);
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) up.cm[j] = tbdetail::in_interior(g.gy0 + col + j, g.ny);
+  }
+  int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last step stores)
+  opaque(off0);
+  const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+  // One step: publish this wave's first and last rows, barrier, fetch the
+  // neighbours' (double-buffered by step parity: one barrier per step).
+  auto xstep = [&](auto down_c, auto last_c, int s) {
+    const int p = s & 1;
+    xch[p][0][w][lane] = T.u[0];
+    xch[p][1][w][lane] = T.u[R - 1];
+    lds_barrier();
+    const vecf above = xch[p][1][wa][lane];
+    const vecf below = xch[p][0][wb][lane];
+    opaque(rowmask);
+    opaque(usemask);
+    T.template step<decltype(down_c)::value, decltype(last_c)::value>(
+        above, below, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch);
+  };
+  using Down = std::true_type;
+  using Up = std::false_type;
+  // Steps in (down, up) pairs (K is even, see launch()); the residual rides
+  // on the last up step.
+  int s = 0;
+  for (; s + 2 < K; s += 2) {
+    xstep(Down{}, std::false_type{}, s);
+    xstep(Up{}, std::false_type{}, s + 1);
+  }
+  xstep(Down{}, std::false_type{}, s);
+  xstep(Up{}, std::true_type{}, s + 1);
+  return T.m;
+}
+
+// Register budget: waves per SIMD each instantiation must fit.
+template <int R, int NW>
+constexpr int tile_waves_per_simd() {
+  return NW >= 16 ? 4 : R <= 16 ? 4 : 2;
+}
+
+template <int R, int NW, bool BP>
+__global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_kernel(TbArgs a, int K) {
+  __shared__ vecf xch[2][2][NW][64];  // [step parity][first / last row][wave][lane]
+  if (tbdetail::gated(a.g.gate)) return;  // uniform over the launch
+  int blk = blockIdx.x;
+  if (a.flags & tbdetail::kTbXcdGroups) {
+    // Contiguous unit ranges per XCD (blocks b, b+8, ... share one XCD):
+    // vertically adjacent tiles of a strip share their K halo rows in L2.
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = blk & 7, j = blk >> 3;
+    blk = x * q + min(x, r) + j;
+  }
+  if (blk >= a.total_waves) return;  // whole workgroup: no barrier is left waiting
+  int bi = 0;
+#pragma unroll
+  for (int j = 1; j < tbdetail::kMaxBoxes; ++j)
+    if (j < a.nbox && blk >= a.box[j].wave_begin) bi = j;
+  const TbBox& bx = a.box[bi];
+  const int u = blk - bx.wave_begin;
+  const int strip = u / bx.nchunks, t = u % bx.nchunks;
+  const StencilGeom& g = a.g;
+  // Tile-uniform Dirichlet mode (every wave of the block takes the same path).
+  const int KK = (K + 3) & ~3;
+  const int64_t cbase = bx.c0 + int64_t(strip) * (256 - 2 * KK);
+  const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
+  const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
+  const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
+  const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
+  float m;
+  if (interior) {
+    m = a.resid ? tile_run<R, NW, 0, true, BP>(a, bx, strip, t, K, xch)
+                : tile_run<R, NW, 0, false, BP>(a, bx, strip, t, K, xch);
+  } else {
+    m = a.resid ? tile_run<R, NW, 1, true, BP>(a, bx, strip, t, K, xch)
+                : tile_run<R, NW, 1, false, BP>(a, bx, strip, t, K, xch);
+  }
+  if (a.resid != nullptr) tbdetail::wave_max_atomic(__float_as_uint(m), a.resid);
+}
+
+template <int R, int NW, bool BP>
+void launch_r(const TbArgs& args, int depth, hipStream_t st) {
+  hipLaunchKernelGGL((tile_kernel<R, NW, BP>), dim3(args.total_waves), dim3(64 * NW), 0, st, args,
+                     depth);
+}
+
+template <int R, int NW, bool BP>
+int occ_r() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_kernel<R, NW, BP>, 64 * NW, 0) != hipSuccess)
+    n = 1;
+  // Bound by the VGPR granule as well (the API can over-report by one block).
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_kernel<R, NW, BP>)) == hipSuccess &&
+      fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    n = std::min(n, (512 / alloc) / (NW / 4));
+  }
+  return std::max(1, n);
+}
+
+// Instantiated (rows per wave, waves per workgroup).
+#define HEAT_TILE_SHAPES(X) X(12, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
+
+bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, hipStream_t st) {
+  if (depth < 2 || depth % 2 != 0 || waves * rows <= 2 * depth) return false;
+#define HEAT_TILE_CASE(r, nw)                                      \
+  if (rows == r && waves == nw) {                                  \
+    if (bpermute) launch_r<r, nw, true>(args, depth, st);          \
+    else launch_r<r, nw, false>(args, depth, st);                  \
+    return true;                                                   \
+  }
+  HEAT_TILE_SHAPES(HEAT_TILE_CASE)
+#undef HEAT_TILE_CASE
+  return false;
+}
+
+int occupancy(int rows, int waves, bool bpermute) {
+#define HEAT_TILE_CASE(r, nw) \
+  if (rows == r && waves == nw) return bpermute ? occ_r<r, nw, true>() : occ_r<r, nw, false>();
+  HEAT_TILE_SHAPES(HEAT_TILE_CASE)
+#undef HEAT_TILE_CASE
+  return 0;
+}
+
+namespace {
+bool trace_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT_TB_TRACE");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+void trace_once(const std::string& line) {
+  static std::mutex mu;
+  static std::set<std::string> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  if (seen.insert(line).second) std::fputs(line.c_str(), stderr);
+}
+// Resident blocks per CU, cached per (device, rows, waves, shifts).
+int cached_occupancy(int rows, int waves, bool bp) {
+  static std::map<std::tuple<int, int, int, bool>, int> cache;
+  static std::mutex mu;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(dev, rows, waves, bp);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  return cache.emplace(key, occupancy(rows, waves, bp)).first->second;
+}
+}  // namespace
+
+// The launch planner.  A tile is one 256-column strip by NW waves x R rows;
+// its useful rows are NW * R - 2 * depth.  The shape comes from the
+// instantiated set by the estimated time of the launch: dispatch rounds x
+// (rows each SIMD updates per round) x (cycles per VALU op at that many
+// waves per SIMD: ~3.0 at 2, ~2.7 at 4 or more,
+// profiles/valu_issue_rate_probe_r1.jsonl).
+void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox, int depth,
+          unsigned* resid, hipStream_t st, int variant, const TbTuning& tune) {
+  struct Shape {
+    int rows, waves;
+  };
+  static constexpr Shape kShapes[] = {{12, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
+  const bool bp = !(variant & tbv::kTileDpp);
+  const int W = tb_strip_width(depth, 4);
+  const int cus = tb_simd_count() / 4;
+  Shape best{0, 0};
+  double best_est = 0.0;
+  for (const Shape& sh : kShapes) {
+    if (tune.tile_rows > 0 && sh.rows != tune.tile_rows) continue;
+    if (tune.tile_waves > 0 && sh.waves != tune.tile_waves) continue;
+    const int64_t hmax = int64_t(sh.waves) * sh.rows - 2 * int64_t(depth);
+    if (hmax < std::max(depth, 4)) continue;
+    int64_t units = 0;
+    for (int b = 0; b < nbox; ++b)
+      if (!boxes[b].empty()) units += ceil_div(boxes[b].cols(), W) * ceil_div(boxes[b].rows(), hmax);
+    const int occ = cached_occupancy(sh.rows, sh.waves, bp);
+    if (occ <= 0) continue;
+    const int per_simd = occ * sh.waves / 4;  // resident waves per SIMD
+    const int64_t rounds = ceil_div(units, int64_t(cus) * occ);
+    const double est = double(rounds) * per_simd * sh.rows * (per_simd >= 4 ? 2.7 : 3.0);
+    if (best.rows == 0 || est < best_est) {
+      best_est = est;
+      best = sh;
+    }
+  }
+  HEAT_CHECK(best.rows > 0, "no tile shape fits depth %d (HEAT_TB_TILE_ROWS=%d, HEAT_TB_TILE_WAVES=%d)",
+             depth, tune.tile_rows, tune.tile_waves);
+  const int64_t hmax = int64_t(best.waves) * best.rows - 2 * int64_t(depth);
+  TbArgs args{};
+  args.src = src;
+  args.dst = dst;
+  args.resid = resid;
+  args.g = g;
+  args.flags = (variant & tbv::kXcdGroups) ? tbdetail::kTbXcdGroups : 0;
+  int n = 0;
+  int64_t units = 0;
+  for (int b = 0; b < nbox; ++b) {
+    const Box& B = boxes[b];
+    if (B.empty()) continue;
+    HEAT_CHECK(B.c0 % 4 == 0, "TB box column start %lld not a multiple of 4", (long long)B.c0);
+    HEAT_CHECK(n < tbdetail::kMaxBoxes, "too many TB boxes");
+    TbBox& t = args.box[n++];
+    t.r0 = B.r0;
+    t.r1 = B.r1;
+    t.c0 = B.c0;
+    t.c1 = B.c1;
+    t.nstrips = int(ceil_div(B.cols(), W));
+    t.nchunks = int(ceil_div(B.rows(), hmax));                 // tiles per strip
+    t.chunk_len = int(ceil_div(B.rows(), int64_t(t.nchunks)));  // useful rows per tile
+    t.wave_begin = int(units);                                  // first unit (block)
+    units += int64_t(t.nstrips) * t.nchunks;
+  }
+  if (n == 0) return;
+  HEAT_CHECK(units < (int64_t(1) << 31), "tile launch too large");
+  args.nbox = n;
+  args.total_waves = int(units);
+  if (trace_enabled()) {
+    char line[200];
+    std::snprintf(line, sizeof line,
+                  "[heat tb] tile depth %d rows %d waves %d bpermute %d boxes %d units %lld tiles0 %d "
+                  "len0 %d\n",
+                  depth, best.rows, best.waves, int(bp), n, (long long)units, args.box[0].nchunks,
+                  args.box[0].chunk_len);
+    trace_once(line);
+  }
+  HEAT_CHECK(launch(args, depth, best.rows, best.waves, bp, st), "tile %dx%d not instantiated",
+             best.rows, best.waves);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace heat::gpu::tbw

@@ -463,6 +463,8 @@ int heat_tb_get_tuning(heat_tb_tuning* out) {
     out->min_len = t.min_len;
     out->waves = t.waves;
     out->edge_frac = t.edge_frac;
+    out->tile_rows = t.tile_rows;
+    out->tile_waves = t.tile_waves;
     out->n_weights = int32_t(std::min<size_t>(t.age_weights.size(), 4));
     for (int i = 0; i < out->n_weights; ++i) out->weights[i] = t.age_weights[size_t(i)];
   });
@@ -478,6 +480,8 @@ int heat_tb_set_tuning(const heat_tb_tuning* in) {
     t.min_len = std::max(0, in->min_len);
     t.waves = std::max(0, in->waves);
     t.edge_frac = in->edge_frac;
+    t.tile_rows = std::max(0, in->tile_rows);
+    t.tile_waves = std::max(0, in->tile_waves);
     t.age_weights.assign(in->weights, in->weights + in->n_weights);
     heat::gpu::tb_set_tuning(t);
   });

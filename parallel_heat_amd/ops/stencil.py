@@ -44,6 +44,8 @@ class TbVariant(enum.IntFlag):
     NO_AGE_PAIRS = 16384  # never age-group
     LINEAR = 32768        # force the balanced plan: equal strip-rows per unit
     NO_LINEAR = 65536     # never switch to it (default: when the classic plan fills < 90 %)
+    TILE = 131072         # workgroup tiles: 8 waves x R rows in VGPRs, LDS row exchange per step
+    TILE_DPP = 262144     # with TILE: DPP lane shifts instead of ds_bpermute
     DEFAULT = RAMP | SCALAR | XCD_GROUPS       # 23
     DEFAULT_DEEP = DEFAULT | SPLIT             # 2071
 
@@ -58,13 +60,15 @@ class TbTuning:
     waves: int = 0
     edge_frac: float = 1.0
     age_weights: List[float] = field(default_factory=list)
+    tile_rows: int = 0  # rows per wave of TILE launches (0: planner)
+    tile_waves: int = 0  # waves per TILE workgroup, 8 or 16 (0: planner)
 
 
 def tb_tuning() -> TbTuning:
     t = _native.HeatTbTuning()
     _native.call("heat_tb_get_tuning", ctypes.byref(t))
     return TbTuning(t.variant, t.rounds, t.min_len, t.waves, t.edge_frac,
-                    [t.weights[i] for i in range(t.n_weights)])
+                    [t.weights[i] for i in range(t.n_weights)], t.tile_rows, t.tile_waves)
 
 
 def set_tb_tuning(t: TbTuning) -> None:
@@ -72,7 +76,8 @@ def set_tb_tuning(t: TbTuning) -> None:
     if n > 4:
         raise ValueError("at most 4 age weights")
     c = _native.HeatTbTuning(int(t.variant), int(t.rounds), int(t.min_len), int(t.waves),
-                             float(t.edge_frac), n, 0, (ctypes.c_double * 4)(*t.age_weights))
+                             float(t.edge_frac), n, int(t.tile_rows),
+                             (ctypes.c_double * 4)(*t.age_weights), int(t.tile_waves), 0)
     _native.call("heat_tb_set_tuning", ctypes.byref(c))
 
 

@@ -9,7 +9,7 @@ def test_tuning_roundtrip():
     saved = ops.tb_tuning()
     try:
         t = ops.TbTuning(variant=int(ops.TbVariant.DEFAULT), rounds=2, min_len=24, waves=512,
-                         edge_frac=0.75, age_weights=[1.5, 1.0])
+                         edge_frac=0.75, age_weights=[1.5, 1.0], tile_rows=16, tile_waves=8)
         ops.set_tb_tuning(t)
         assert ops.tb_tuning() == t
         with pytest.raises(ValueError):
@@ -31,7 +31,8 @@ def test_variant_flags_match_the_engine():
              "kScalar": V.SCALAR, "kXcdGroups": V.XCD_GROUPS, "kAltDirection": V.ALT_DIRECTION,
              "kFloat2": V.FLOAT2, "kForceAgePairs": V.FORCE_AGE_PAIRS, "kSplit": V.SPLIT,
              "kDiagNoStore": V.DIAG_NO_STORE, "kDiagCachedRows": V.DIAG_CACHED_ROWS,
-             "kNoAgePairs": V.NO_AGE_PAIRS, "kLinear": V.LINEAR, "kNoLinear": V.NO_LINEAR}
+             "kNoAgePairs": V.NO_AGE_PAIRS, "kLinear": V.LINEAR, "kNoLinear": V.NO_LINEAR,
+             "kTile": V.TILE, "kTileDpp": V.TILE_DPP}
     for n, v in names.items():
         m = re.search(rf"\b{n} = (\d+),", src)
         assert m and int(m.group(1)) == int(v), n
