@@ -398,8 +398,10 @@ int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
   // (profiles/tb_block_shapes_r2.md).
   // Below ~48 (the 8-GPU blocks 1024 x 8192 and 2048 x 4096 and their
   // deep-halo passes) the workgroup tiles win: +6-7 % over one wave per
-  // chunk; at 54 they lose 8 % (profiles/r3_tile.md).
-  if (depth == kTbDeepDepth && strip_rows_per_simd < 48) return tbv::kTile | tbv::kXcdGroups;
+  // chunk inside the plate, +38 % on blocks with a plate edge (the first and
+  // last rank); at 54 they lose 8 % (profiles/r3_tile.md).  Even depths
+  // only (the tile runs steps in pairs).
+  if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < 48) return tbv::kTile | tbv::kXcdGroups;
   if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
   return tb_default_variant(depth);
 }
