@@ -132,16 +132,19 @@ struct Tile {
   float m = 0.f;
 
   // One time step of this wave's rows, in place, top-down (DOWN) or
-  // bottom-up.  above / below: the last row of the wave above and the first
-  // row of the wave below (old values).  Alternating the direction every step
+  // bottom-up.  first_nb: the outside neighbour of the first row processed
+  // (old value, already in a register); the outside neighbour of the last
+  // row comes from xc.mid(), called halfway through the step (the step's
+  // workgroup barrier), and xc.publish(0 / 1, row) hands the first / last
+  // row computed to the neighbour waves.  Alternating the direction every step
   // lets the register allocator put new row r where old row r -/+ 1 was (dead
   // by then) and be back at the loop's assignment after two steps: one
   // direction only needed a copy of every row per step at the back-edge.
   // LAST: the launch's last step stores every useful row as soon as it is
   // computed (dst + off0 + r * pitch, this lane's columns if store_lane) and,
   // with RES, accumulates max |new - old| over the useful cells.
-  template <bool DOWN, bool LAST>
-  __device__ __forceinline__ void step(const vecf& above, const vecf& below, const Upd<MODE, BP>& up,
+  template <bool DOWN, bool LAST, class Xc>
+  __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, BP>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
                                        float* __restrict__ dst, int64_t off0, int64_t pitch) {
     // Lane shifts of the OLD rows.  ds_bpermute results take ~50+ cycles: the
@@ -161,14 +164,18 @@ struct Tile {
       for (int i = 0; i < PD; ++i) shift(row_at(i));
     }
     vecf prev = u[row_at(0)];  // old value of the row processed before
+    vecf last_nb = first_nb;     // set by xc.mid() before the last row
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int r = row_at(i);
       if (i + PD < R) shift(row_at(i + PD));
       const vecf cur = u[r];
-      const vecf n = r == 0 ? above : (DOWN ? prev : u[r - 1]);
-      const vecf so = r == R - 1 ? below : (DOWN ? u[r + 1] : prev);
+      const vecf outside = i == 0 ? first_nb : last_nb;
+      const vecf n = r == 0 ? outside : (DOWN ? prev : u[r - 1]);
+      const vecf so = r == R - 1 ? outside : (DOWN ? u[r + 1] : prev);
       u[r] = up.apply(n, cur, so, wl[r], er[r], (rowmask >> r) & 1u);
+      if (i == 0) xc.publish(0, u[r]);
+      if (i == R - 1) xc.publish(1, u[r]);
       if constexpr (LAST) {
         if ((usemask >> r) & 1u) {
           if (store_lane) *reinterpret_cast<vecf*>(dst + off0 + r * pitch) = u[r];
@@ -176,6 +183,7 @@ struct Tile {
         }
       }
       prev = cur;
+      if (i == R / 2 - 1) last_nb = xc.mid();
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -249,19 +257,44 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last step stores)
   opaque(off0);
   const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
-  // One step: publish this wave's first and last rows, barrier, fetch the
-  // neighbours' (double-buffered by step parity: one barrier per step).
+  // Neighbour rows through LDS, one workgroup barrier per step placed
+  // HALFWAY through the step.  A step publishes the row it computes first
+  // (early slot E) and the row it computes last (late slot L); with the
+  // direction alternating, the row a wave needs first in step s + 1 is its
+  // neighbour's EARLY row of step s (read right after step s's barrier, so
+  // it waits in a register when step s + 1 starts) and the row it needs last
+  // is the neighbour's LATE row of step s (read after step s + 1's barrier).
+  // A barrier at the step boundary left every wave of the workgroup waiting
+  // on the LDS read of its first row at once.  Slots are double-buffered by
+  // step parity; each is rewritten only after the barrier that follows its
+  // readers' use.
+  struct Xc {
+    vecf (*xch)[2][NW][64];
+    int w, lane, p, last_w, next_w;
+    vecf efirst;
+    __device__ __forceinline__ void publish(int late, const vecf& v) { xch[p][late][w][lane] = v; }
+    __device__ __forceinline__ vecf mid() {
+      lds_barrier();
+      const vecf l = xch[p ^ 1][1][last_w][lane];  // neighbour's late row of step s - 1
+      efirst = xch[p][0][next_w][lane];             // neighbour's early row of step s
+      return l;
+    }
+  } xc{xch, w, lane, 1, 0, 0, vecf{}};
+  // Step -1 (fictional, bottom-up): early row R - 1, late row 0.
+  xch[1][0][w][lane] = T.u[R - 1];
+  xch[1][1][w][lane] = T.u[0];
+  lds_barrier();
+  xc.efirst = xch[1][0][wa][lane];
   auto xstep = [&](auto down_c, auto last_c, int s) {
-    const int p = s & 1;
-    xch[p][0][w][lane] = T.u[0];
-    xch[p][1][w][lane] = T.u[R - 1];
-    lds_barrier();
-    const vecf above = xch[p][1][wa][lane];
-    const vecf below = xch[p][0][wb][lane];
+    constexpr bool D = decltype(down_c)::value;
+    xc.p = s & 1;
+    // Down: the last row needs the wave below; so does the next (up) step's first.
+    xc.last_w = xc.next_w = D ? wb : wa;
+    const vecf first_nb = xc.efirst;
     opaque(rowmask);
     opaque(usemask);
-    T.template step<decltype(down_c)::value, decltype(last_c)::value>(
-        above, below, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch);
+    T.template step<D, decltype(last_c)::value>(first_nb, xc, up, rowmask, usemask, store_lane, rc,
+                                                 dst + lo, off0, pitch);
   };
   using Down = std::true_type;
   using Up = std::false_type;
