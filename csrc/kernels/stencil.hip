@@ -396,12 +396,14 @@ int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
   // 8192, 2048 x 4096, 1536 x 8192, ...) one wave per (strip, chunk) at
   // depth 12 is 8-12 % faster, above it the split is 2-4 % faster
   // (profiles/tb_block_shapes_r2.md).
-  // Below ~48 (the 8-GPU blocks 1024 x 8192 and 2048 x 4096 and their
-  // deep-halo passes) the workgroup tiles win: +6-7 % over one wave per
-  // chunk inside the plate, +38 % on blocks with a plate edge (the first and
-  // last rank); at 54 they lose 8 % (profiles/r3_tile.md).  Even depths
-  // only (the tile runs steps in pairs).
-  if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < 48) return tbv::kTile | tbv::kXcdGroups;
+  // Below 64 (the 8-GPU blocks 1024 x 8192 and 2048 x 4096 and their
+  // deep-halo passes, 1536-row blocks) the workgroup tiles win: +6-10 % over
+  // one wave per chunk inside the plate at 36, and +36-38 % on blocks with a
+  // plate edge (the first and last rank, whose time the max over ranks
+  // reports) at 36 and 54, where one wave per chunk loses 8 % inside the
+  // plate (profiles/r3_tile.md).  Even depths only (the tile runs steps in
+  // pairs).  From 64 the split pipelines keep the edge ranks within 2 %.
+  if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < 64) return tbv::kTile | tbv::kXcdGroups;
   if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
   return tb_default_variant(depth);
 }
