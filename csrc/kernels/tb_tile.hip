@@ -376,7 +376,7 @@ int occ_r() {
 }
 
 // Instantiated (rows per wave, waves per workgroup).
-#define HEAT_TILE_SHAPES(X) X(12, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
+#define HEAT_TILE_SHAPES(X) X(12, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
 
 bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, hipStream_t st) {
   if (depth < 2 || depth % 2 != 0 || waves * rows <= 2 * depth) return false;
@@ -438,7 +438,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
   struct Shape {
     int rows, waves;
   };
-  static constexpr Shape kShapes[] = {{12, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
+  static constexpr Shape kShapes[] = {{12, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
   const bool bp = !(variant & tbv::kTileDpp);
   const int W = tb_strip_width(depth, 4);
   const int cus = tb_simd_count() / 4;
