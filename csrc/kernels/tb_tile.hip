@@ -376,7 +376,7 @@ int occ_r() {
 }
 
 // Instantiated (rows per wave, waves per workgroup).
-#define HEAT_TILE_SHAPES(X) X(12, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
+#define HEAT_TILE_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
 
 bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, hipStream_t st) {
   if (depth < 2 || depth % 2 != 0 || waves * rows <= 2 * depth) return false;
@@ -430,15 +430,16 @@ int cached_occupancy(int rows, int waves, bool bp) {
 // The launch planner.  A tile is one 256-column strip by NW waves x R rows;
 // its useful rows are NW * R - 2 * depth.  The shape comes from the
 // instantiated set by the estimated time of the launch: dispatch rounds x
-// (rows each SIMD updates per round) x (cycles per VALU op at that many
-// waves per SIMD: ~3.0 at 2, ~2.7 at 4 or more,
-// profiles/valu_issue_rate_probe_r1.jsonl).
+// (rows each SIMD updates per round) x (relative cycles per VALU op: 2.7
+// with two or more independent workgroups per CU, 3.1 with one, whose waves
+// stall together at its barriers; calibrated on the 8-GPU blocks,
+// profiles/r3_tile.md).
 void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox, int depth,
           unsigned* resid, hipStream_t st, int variant, const TbTuning& tune) {
   struct Shape {
     int rows, waves;
   };
-  static constexpr Shape kShapes[] = {{12, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
+  static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
   const bool bp = !(variant & tbv::kTileDpp);
   const int W = tb_strip_width(depth, 4);
   const int cus = tb_simd_count() / 4;
@@ -456,7 +457,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
     if (occ <= 0) continue;
     const int per_simd = occ * sh.waves / 4;  // resident waves per SIMD
     const int64_t rounds = ceil_div(units, int64_t(cus) * occ);
-    const double est = double(rounds) * per_simd * sh.rows * (per_simd >= 4 ? 2.7 : 3.0);
+    const double est = double(rounds) * per_simd * sh.rows * (occ >= 2 ? 2.7 : 3.1);
     if (best.rows == 0 || est < best_est) {
       best_est = est;
       best = sh;

@@ -35,7 +35,7 @@ def tile_rows():
     ops.set_tb_tuning(saved)
 
 
-SHAPES = [(12, 8), (14, 8), (16, 8), (20, 8), (24, 8), (28, 8), (32, 8), (12, 16)]
+SHAPES = [(12, 8), (13, 8), (14, 8), (16, 8), (20, 8), (24, 8), (28, 8), (32, 8), (12, 16)]
 
 
 @pytest.mark.parametrize("variant", [TILE, TILE_DPP])
