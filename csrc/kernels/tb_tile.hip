@@ -8,15 +8,17 @@
 // wave per SIMD, which issues a VALU op every ~4-6 cycles instead of ~2-3
 // (profiles/r3_small_blocks.md).
 //
-// Here a workgroup of NW = 8 (or 16) waves owns one tile: a 256-column strip (64 lanes
-// x float4) by NW * R rows, every wave R consecutive rows held in VGPRs for
-// the whole launch.  A time step updates all rows in place; the only data a
-// wave needs from outside its registers are the last row of the wave above
-// and the first row of the wave below, exchanged through LDS (one barrier per
-// step, double-buffered slots).  So the tile pays only its own K-deep ghost
-// ring (2K of NW * R rows, round_up(K, 4) columns per side) instead of a
-// trapezoid per wave, and runs two (R >= 20) or four (R <= 16) waves per SIMD.
-// East/west neighbours cross lanes with ds_bpermute (BP) or DPP wave shifts.
+// Here a workgroup of NW = 8 (or 16) waves owns one tile: a 256-column strip
+// (64 lanes x float4) by NW * R rows, every wave R consecutive rows held in
+// VGPRs for the whole launch.  A time step updates all rows in place; the
+// only data a wave needs from outside its registers are the last row of the
+// wave above and the first row of the wave below, exchanged through LDS (one
+// barrier per step, halfway through it, see tile_run).  The tile pays its
+// own K-deep ghost ring (2K of NW * R rows, round_up(K, 4) columns per side)
+// instead of a trapezoid per wave -- about the same VALU work -- but runs
+// 2-4 waves per SIMD (two workgroups per CU up to R = 16) where the
+// streaming kernel has room for one (profiles/r3_tile.md).  East/west
+// neighbours cross lanes with ds_bpermute (BP) or DPP wave shifts.
 //
 // Input rows [r0 - K, r1 + K) and columns [c0 - round_up(K, 4), ...) of each
 // box are read (the same footprint as tb_stream.inl); rows of the tile past
