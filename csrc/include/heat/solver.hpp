@@ -133,6 +133,9 @@ class Solver {
   void free_all();
   void init_fields();
   std::vector<int> pass_depths(int64_t n) const;
+  // Every rank's depth-T launches are small enough for the workgroup-tile
+  // kernel (even depths): remainder passes are then split into even parts.
+  bool tile_sized() const;
   // Passes for steps [step0, step0+n), cut at every check point (the
   // residual is the last level of its pass).
   std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;

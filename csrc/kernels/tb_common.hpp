@@ -89,6 +89,24 @@ __device__ __forceinline__ void wave_max_atomic(unsigned m, unsigned* resid) {
   if ((threadIdx.x & 63) == 0) atomicMax(resid, m);
 }
 
+// The same with ONE global atomic per workgroup: every contributing wave
+// folds its max into an LDS word wg[0] and counts itself in wg[1]; the last
+// of the nact contributors (LDS requests of a wave execute in order, so all
+// earlier folds are in) publishes.  Per-wave atomics on the one residual word
+// from thousands of waves serialise at the memory side (~7 ns each: ~37 us
+// per check pass at 4000 waves).  No barrier: waves of the block may have
+// exited already.  wg must be zeroed (and a barrier passed) at kernel start.
+__device__ __forceinline__ void group_max_atomic(unsigned m, unsigned* resid, unsigned* wg, int nact) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = max(m, unsigned(__shfl_xor(int(m), off)));
+  if ((threadIdx.x & 63) == 0) {
+    __hip_atomic_fetch_max(wg, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned n = __hip_atomic_fetch_add(wg + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (int(n) == nact - 1)
+      atomicMax(resid, __hip_atomic_load(wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  }
+}
+
 }  // namespace heat::gpu::tbdetail
 
 namespace heat::gpu::tbp {

@@ -665,7 +665,7 @@ __device__ __forceinline__ int64_t tb_lin_boundary(const TbArgs& a, int64_t x) {
 // or a row where the Dirichlet mode changes starts a new segment).
 template <int K, int LAG, int K1>
 __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
-                                       unsigned* cnt) {
+                                       unsigned* cnt, unsigned* wg, int nact) {
   constexpr int K2 = K - K1;
   const int lane = threadIdx.x & 63;
   const bool pairs = a.flags & tbdetail::kTbAgePairs;
@@ -733,7 +733,8 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       qoff += (re - rb) + 2 * K2;
     }
   }
-  if (a.resid != nullptr && (K1 == 0 || stage == 1)) wave_max_atomic(__float_as_uint(m), a.resid);
+  if (a.resid != nullptr && (K1 == 0 || stage == 1))
+    tbdetail::group_max_atomic(__float_as_uint(m), a.resid, wg, nact);
   if (a.stamps && lane == 0) {
     const int64_t idx = int64_t(wave) + int64_t(age) * a.total_waves;
     unsigned long long* st = a.stamps + 4 * (K1 == 0 ? idx : 2 * idx + stage);
@@ -749,11 +750,20 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
 
 template <int K, int LAG>
 __global__ __launch_bounds__(256, (tb_waves_per_simd<K, LAG>())) void tb_kernel(TbArgs a) {
+  __shared__ unsigned wg[2];  // residual: block max, contributors done
   if (tbdetail::gated(a.g.gate)) return;
+  if (threadIdx.x < 2) wg[threadIdx.x] = 0u;
+  __syncthreads();
   int age = 0;
   const int wave = tb_unit(a, 4, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), age);
+  int nact = 0;  // waves of this block with a unit (all contribute a residual)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    int ag = 0;
+    nact += tb_unit(a, 4, s, ag) < a.total_waves ? 1 : 0;
+  }
   if (wave >= a.total_waves) return;
-  tb_run<K, LAG, 0>(a, wave, age, 0, nullptr, nullptr);
+  tb_run<K, LAG, 0>(a, wave, age, 0, nullptr, nullptr, wg, nact);
 }
 
 #if HEAT_TB_SPLIT
@@ -771,15 +781,23 @@ template <int K, int K1>
 __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_split_kernel(TbArgs a) {
   __shared__ vecf ring[2][kSplitRing * 64];
   __shared__ unsigned cnt[2][2];
+  __shared__ unsigned wg[2];  // residual: block max, contributors done
   if (tbdetail::gated(a.g.gate)) return;  // the same value for every wave of the block
   if (threadIdx.x < 4) cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  if (threadIdx.x < 2) wg[threadIdx.x] = 0u;
   __syncthreads();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = wid >> 1;
   int age = 0;
   const int unit = tb_unit(a, 2, p, age);
+  int nact = 0;  // pipelines of this block with a unit (their stage-1 wave contributes)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    int ag = 0;
+    nact += tb_unit(a, 2, q, ag) < a.total_waves ? 1 : 0;
+  }
   if (unit >= a.total_waves) return;
-  tb_run<K, 3, K1>(a, unit, age, wid & 1, ring[p], cnt[p]);
+  tb_run<K, 3, K1>(a, unit, age, wid & 1, ring[p], cnt[p], wg, nact);
 }
 #endif
 

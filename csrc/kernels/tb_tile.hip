@@ -353,7 +353,24 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
     m = a.resid ? tile_run<R, NW, 1, true, BP>(a, bx, strip, t, K, xch)
                 : tile_run<R, NW, 1, false, BP>(a, bx, strip, t, K, xch);
   }
-  if (a.resid != nullptr) tbdetail::wave_max_atomic(__float_as_uint(m), a.resid);
+  if (a.resid != nullptr) {
+    // One atomic per workgroup: a per-wave atomicMax on the one residual
+    // word from ~4000 waves serialised at the memory side (~37 us per check
+    // pass at 1024 x 8192, as much as the whole pass).  Non-negative floats
+    // (and NaN, sign cleared by fabs) order like their bit patterns.
+    __shared__ unsigned wmax[NW];
+    unsigned mm = __float_as_uint(m);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mm = max(mm, unsigned(__shfl_xor(int(mm), off)));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned r = 0u;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) r = max(r, wmax[i]);
+      atomicMax(a.resid, r);
+    }
+  }
 }
 
 template <int R, int NW, bool BP>

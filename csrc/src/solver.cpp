@@ -252,6 +252,19 @@ int Solver::auto_tb_depth() const {
   return min_lx >= 1024 ? gpu::kTbDeepDepth : 8;
 }
 
+bool Solver::tile_sized() const {
+  // The same rule as gpu::tb_auto_variant (strip-rows per SIMD of the owned
+  // block), decided from the largest block of any rank so that every rank
+  // plans the same passes.
+  if (!on_gpu() || !tb_kernel()) return false;
+  const int64_t W = gpu::tb_strip_width(T_, 4), simds = gpu::tb_simd_count();
+  for (int r = 0; r < cart_.world; ++r) {
+    const Block b = make_block(cart_, r, P_.nx, P_.ny);
+    if (ceil_div(b.ly, W) * b.lx >= 64 * simds) return false;
+  }
+  return true;
+}
+
 std::vector<int> Solver::pass_depths(int64_t n) const {
   std::vector<int> d;
   const bool tb = tb_kernel();
@@ -269,7 +282,16 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
         total += T_;
       }
       const int parts = (total + gpu::kTbMaxDepth - 1) / gpu::kTbMaxDepth;
-      for (int i = 0; i < parts; ++i) d.push_back(total / parts + (i < total % parts ? 1 : 0));
+      if (total % 2 == 0 && tile_sized()) {
+        // Even parts where the total allows (a 50-step check period is
+        // 12,12,12,8,6, not 12,12,12,7,7): the workgroup-tile kernel of
+        // small launches runs steps in pairs, and an odd pass would stream
+        // (large launches keep 7,7: a depth-6 streaming pass costs more).
+        const int pairs = total / 2;
+        for (int i = 0; i < parts; ++i) d.push_back(2 * (pairs / parts + (i < pairs % parts ? 1 : 0)));
+      } else {
+        for (int i = 0; i < parts; ++i) d.push_back(total / parts + (i < total % parts ? 1 : 0));
+      }
     }
     return d;
   }
