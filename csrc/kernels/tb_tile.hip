@@ -18,7 +18,7 @@
 // instead of a trapezoid per wave -- about the same VALU work -- but runs
 // 2-4 waves per SIMD (two workgroups per CU up to R = 16) where the
 // streaming kernel has room for one (profiles/r3_tile.md).  East/west
-// neighbours cross lanes with ds_bpermute (BP) or DPP wave shifts.
+// neighbours cross lanes with ds_bpermute (XL) or DPP wave shifts.
 //
 // Input rows [r0 - K, r1 + K) and columns [c0 - round_up(K, 4), ...) of each
 // box are read (the same footprint as tb_stream.inl); rows of the tile past
@@ -53,19 +53,21 @@ typedef float vecf __attribute__((ext_vector_type(4)));
 #endif
 
 // Lane l <- lane l-1 / l+1.  Lanes 0 and 63 lie in the strip overlap
-// (don't-care values).
-template <bool BP>
+// (don't-care values).  XL: 0 both shifts DPP wave shifts (folded into the
+// e + w add), 1 both ds_bpermute (issued PD rows ahead), 2 mixed: the left
+// shift DPP, the right one ds_bpermute (half the LDS-crossbar issue).
+template <int XL>
 __device__ __forceinline__ float from_left(float v) {
-  if constexpr (BP) {
+  if constexpr (XL == 1) {
     const int l = threadIdx.x & 63;
     return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 63) & 63) << 2, __float_as_int(v)));
   } else {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
   }
 }
-template <bool BP>
+template <int XL>
 __device__ __forceinline__ float from_right(float v) {
-  if constexpr (BP) {
+  if constexpr (XL >= 1) {
     const int l = threadIdx.x & 63;
     return __int_as_float(__builtin_amdgcn_ds_bpermute(((l + 1) & 63) << 2, __float_as_int(v)));
   } else {
@@ -103,7 +105,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 // MODE 0: no cell of the tile is on the plate's fixed ring (or outside it);
 // MODE 1: per-lane column masks and a per-row (uniform) mask keep those cells.
-template <int MODE, bool BP>
+template <int MODE, int XL>
 struct Upd {
   float cx, cy;
   bool cm[4];
@@ -128,7 +130,7 @@ struct Upd {
   }
 };
 
-template <int R, int MODE, bool RES, bool BP>
+template <int R, int MODE, bool RES, int XL>
 struct Tile {
   vecf u[R];
   float m = 0.f;
@@ -146,7 +148,7 @@ struct Tile {
   // computed (dst + off0 + r * pitch, this lane's columns if store_lane) and,
   // with RES, accumulates max |new - old| over the useful cells.
   template <bool DOWN, bool LAST, class Xc>
-  __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, BP>& up,
+  __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, XL>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
                                        float* __restrict__ dst, int64_t off0, int64_t pitch) {
     // Lane shifts of the OLD rows.  ds_bpermute results take ~50+ cycles: the
@@ -154,14 +156,14 @@ struct Tile {
     // a row is computed (scheduling barriers keep that order; unconstrained,
     // the scheduler hoisted every row's shifts and spilled).  DPP shifts fold
     // into the add.
-    constexpr int PD = BP ? (R - 1 < HEAT_TILE_PD ? R - 1 : HEAT_TILE_PD) : 0;
+    constexpr int PD = XL >= 1 ? (R - 1 < HEAT_TILE_PD ? R - 1 : HEAT_TILE_PD) : 0;
     float wl[R], er[R];
     auto row_at = [](int i) { return DOWN ? i : R - 1 - i; };
-    auto shift = [&](int r) {
-      wl[r] = from_left<BP>(u[r][3]);
-      er[r] = from_right<BP>(u[r][0]);
+    auto shift = [&](int r) {  // the ds_bpermute shifts, issued ahead
+      if constexpr (XL == 1) wl[r] = from_left<XL>(u[r][3]);
+      if constexpr (XL >= 1) er[r] = from_right<XL>(u[r][0]);
     };
-    if constexpr (BP) {
+    if constexpr (XL >= 1) {
 #pragma unroll
       for (int i = 0; i < PD; ++i) shift(row_at(i));
     }
@@ -170,7 +172,9 @@ struct Tile {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int r = row_at(i);
-      if (i + PD < R) shift(row_at(i + PD));
+      if (XL >= 1 && i + PD < R) shift(row_at(i + PD));
+      if constexpr (XL != 1) wl[r] = from_left<XL>(u[r][3]);
+      if constexpr (XL == 0) er[r] = from_right<XL>(u[r][0]);
       const vecf cur = u[r];
       const vecf outside = i == 0 ? first_nb : last_nb;
       const vecf n = r == 0 ? outside : (DOWN ? prev : u[r - 1]);
@@ -203,7 +207,7 @@ struct Tile {
   }
 };
 
-template <int R, int NW, int MODE, bool RES, bool BP>
+template <int R, int NW, int MODE, bool RES, int XL>
 __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int strip, int t, int K,
                                           vecf (*xch)[2][NW][64]) {
   const int lane = threadIdx.x & 63;
@@ -225,7 +229,7 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   float* __restrict__ dst = a.dst + (cbase - KK);
   const int lo = 4 * lane;
 
-  Tile<R, MODE, RES, BP> T;
+  Tile<R, MODE, RES, XL> T;
   // Row offsets are made opaque (asm) so the compiler neither keeps R 64-bit
   // row offsets alive from the loads to the stores (CSE) nor hoists per-row
   // masks out of the step loop: both spilled SGPRs into VGPR lanes.
@@ -240,7 +244,7 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
 #pragma unroll
   for (int r = 1; r < R - 1; ++r) T.u[r] = ld(r);
 
-  Upd<MODE, BP> up;
+  Upd<MODE, XL> up;
   up.cx = to_vgpr(g.cx);
   up.cy = to_vgpr(g.cy);
   // Bit r: row row0 + r is a global interior row (MODE 1) / a useful row.
@@ -318,7 +322,7 @@ constexpr int tile_waves_per_simd() {
   return NW >= 16 ? 4 : R <= 16 ? 4 : 2;
 }
 
-template <int R, int NW, bool BP>
+template <int R, int NW, int XL>
 __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_kernel(TbArgs a, int K) {
   __shared__ vecf xch[2][2][NW][64];  // [step parity][first / last row][wave][lane]
   if (tbdetail::gated(a.g.gate)) return;  // uniform over the launch
@@ -347,11 +351,11 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
   float m;
   if (interior) {
-    m = a.resid ? tile_run<R, NW, 0, true, BP>(a, bx, strip, t, K, xch)
-                : tile_run<R, NW, 0, false, BP>(a, bx, strip, t, K, xch);
+    m = a.resid ? tile_run<R, NW, 0, true, XL>(a, bx, strip, t, K, xch)
+                : tile_run<R, NW, 0, false, XL>(a, bx, strip, t, K, xch);
   } else {
-    m = a.resid ? tile_run<R, NW, 1, true, BP>(a, bx, strip, t, K, xch)
-                : tile_run<R, NW, 1, false, BP>(a, bx, strip, t, K, xch);
+    m = a.resid ? tile_run<R, NW, 1, true, XL>(a, bx, strip, t, K, xch)
+                : tile_run<R, NW, 1, false, XL>(a, bx, strip, t, K, xch);
   }
   if (a.resid != nullptr) {
     // One atomic per workgroup: a per-wave atomicMax on the one residual
@@ -373,20 +377,20 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   }
 }
 
-template <int R, int NW, bool BP>
+template <int R, int NW, int XL>
 void launch_r(const TbArgs& args, int depth, hipStream_t st) {
-  hipLaunchKernelGGL((tile_kernel<R, NW, BP>), dim3(args.total_waves), dim3(64 * NW), 0, st, args,
+  hipLaunchKernelGGL((tile_kernel<R, NW, XL>), dim3(args.total_waves), dim3(64 * NW), 0, st, args,
                      depth);
 }
 
-template <int R, int NW, bool BP>
+template <int R, int NW, int XL>
 int occ_r() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_kernel<R, NW, BP>, 64 * NW, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_kernel<R, NW, XL>, 64 * NW, 0) != hipSuccess)
     n = 1;
   // Bound by the VGPR granule as well (the API can over-report by one block).
   hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_kernel<R, NW, BP>)) == hipSuccess &&
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_kernel<R, NW, XL>)) == hipSuccess &&
       fa.numRegs > 0) {
     const int alloc = (fa.numRegs + 7) / 8 * 8;
     n = std::min(n, (512 / alloc) / (NW / 4));
@@ -397,12 +401,14 @@ int occ_r() {
 // Instantiated (rows per wave, waves per workgroup).
 #define HEAT_TILE_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
 
-bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, hipStream_t st) {
+namespace {
+bool launch_xl(const TbArgs& args, int depth, int rows, int waves, int xl, hipStream_t st) {
   if (depth < 2 || depth % 2 != 0 || waves * rows <= 2 * depth) return false;
 #define HEAT_TILE_CASE(r, nw)                                      \
   if (rows == r && waves == nw) {                                  \
-    if (bpermute) launch_r<r, nw, true>(args, depth, st);          \
-    else launch_r<r, nw, false>(args, depth, st);                  \
+    if (xl == 1) launch_r<r, nw, 1>(args, depth, st);              \
+    else if (xl == 2) launch_r<r, nw, 2>(args, depth, st);         \
+    else launch_r<r, nw, 0>(args, depth, st);                      \
     return true;                                                   \
   }
   HEAT_TILE_SHAPES(HEAT_TILE_CASE)
@@ -410,13 +416,21 @@ bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, h
   return false;
 }
 
-int occupancy(int rows, int waves, bool bpermute) {
-#define HEAT_TILE_CASE(r, nw) \
-  if (rows == r && waves == nw) return bpermute ? occ_r<r, nw, true>() : occ_r<r, nw, false>();
+int occupancy_xl(int rows, int waves, int xl) {
+#define HEAT_TILE_CASE(r, nw)                                                           \
+  if (rows == r && waves == nw)                                                         \
+    return xl == 1 ? occ_r<r, nw, 1>() : xl == 2 ? occ_r<r, nw, 2>() : occ_r<r, nw, 0>();
   HEAT_TILE_SHAPES(HEAT_TILE_CASE)
 #undef HEAT_TILE_CASE
   return 0;
 }
+}  // namespace
+
+bool launch(const TbArgs& args, int depth, int rows, int waves, bool bpermute, hipStream_t st) {
+  return launch_xl(args, depth, rows, waves, bpermute ? 1 : 0, st);
+}
+
+int occupancy(int rows, int waves, bool bpermute) { return occupancy_xl(rows, waves, bpermute ? 1 : 0); }
 
 namespace {
 bool trace_enabled() {
@@ -433,8 +447,8 @@ void trace_once(const std::string& line) {
   if (seen.insert(line).second) std::fputs(line.c_str(), stderr);
 }
 // Resident blocks per CU, cached per (device, rows, waves, shifts).
-int cached_occupancy(int rows, int waves, bool bp) {
-  static std::map<std::tuple<int, int, int, bool>, int> cache;
+int cached_occupancy(int rows, int waves, int bp) {
+  static std::map<std::tuple<int, int, int, int>, int> cache;
   static std::mutex mu;
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
@@ -442,7 +456,7 @@ int cached_occupancy(int rows, int waves, bool bp) {
   const auto key = std::make_tuple(dev, rows, waves, bp);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  return cache.emplace(key, occupancy(rows, waves, bp)).first->second;
+  return cache.emplace(key, occupancy_xl(rows, waves, bp)).first->second;
 }
 }  // namespace
 
@@ -459,7 +473,13 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
     int rows, waves;
   };
   static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
-  const bool bp = !(variant & tbv::kTileDpp);
+  // Lane shifts: ds_bpermute (1) unless the variant asks for DPP (0);
+  // HEAT_TB_TILE_XL=0/1/2 overrides (2: mixed, A/B only).
+  static const int xl_env = [] {
+    const char* e = std::getenv("HEAT_TB_TILE_XL");
+    return e && *e ? std::atoi(e) : -1;
+  }();
+  const int bp = xl_env >= 0 && xl_env <= 2 ? xl_env : (variant & tbv::kTileDpp) ? 0 : 1;
   const int W = tb_strip_width(depth, 4);
   const int cus = tb_simd_count() / 4;
   Shape best{0, 0};
@@ -522,7 +542,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
                   args.box[0].chunk_len);
     trace_once(line);
   }
-  HEAT_CHECK(launch(args, depth, best.rows, best.waves, bp, st), "tile %dx%d not instantiated",
+  HEAT_CHECK(launch_xl(args, depth, best.rows, best.waves, bp, st), "tile %dx%d not instantiated",
              best.rows, best.waves);
   HIP_CHECK(hipGetLastError());
 }
