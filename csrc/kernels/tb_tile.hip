@@ -18,7 +18,7 @@
 // instead of a trapezoid per wave -- about the same VALU work -- but runs
 // 2-4 waves per SIMD (two workgroups per CU up to R = 16) where the
 // streaming kernel has room for one (profiles/r3_tile.md).  East/west
-// neighbours cross lanes with ds_bpermute (XL) or DPP wave shifts.
+// neighbours cross lanes with DPP wave shifts and / or ds_bpermute (XL).
 //
 // Input rows [r0 - K, r1 + K) and columns [c0 - round_up(K, 4), ...) of each
 // box are read (the same footprint as tb_stream.inl); rows of the tile past
@@ -473,13 +473,15 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
     int rows, waves;
   };
   static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
-  // Lane shifts: ds_bpermute (1) unless the variant asks for DPP (0);
-  // HEAT_TB_TILE_XL=0/1/2 overrides (2: mixed, A/B only).
+  // Lane shifts: mixed (2: the left shift a DPP wave shift folded into the
+  // add, the right one ds_bpermute issued ahead; +3-6 % over ds_bpermute for
+  // both, which waited on LDS issue 13 % of the time, profiles/r3_tile.md)
+  // unless the variant asks for DPP (0); HEAT_TB_TILE_XL=0/1/2 overrides.
   static const int xl_env = [] {
     const char* e = std::getenv("HEAT_TB_TILE_XL");
     return e && *e ? std::atoi(e) : -1;
   }();
-  const int bp = xl_env >= 0 && xl_env <= 2 ? xl_env : (variant & tbv::kTileDpp) ? 0 : 1;
+  const int bp = xl_env >= 0 && xl_env <= 2 ? xl_env : (variant & tbv::kTileDpp) ? 0 : 2;
   const int W = tb_strip_width(depth, 4);
   const int cus = tb_simd_count() / 4;
   Shape best{0, 0};
