@@ -32,13 +32,18 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp
 	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -x hip -c $< -o $@
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
-$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o \
+  $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -c $< -o $@
 
 -include $(OBJS:.o=.d)
+# An object without its .d file (built before -MMD, or never built) depends
+# on every header: a shared-header edit can never link objects built against
+# two layouts of one struct (TbArgs).
+$(foreach o,$(OBJS),$(if $(wildcard $(o:.o=.d)),,$(eval $(o): $(HDRS) $(KHDRS))))
 
 $(LIBDIR)/libheat.so: $(OBJS)
 	@mkdir -p $(LIBDIR)

@@ -53,10 +53,12 @@ void usage() {
       "  --numerics fp32|mpi     update arithmetic (mpi = reference MPI double) [fp32]\n"
       "  --checkpoint PATH --checkpoint-every K   periodic binary checkpoints\n"
       "  --resume PATH           start from a binary checkpoint\n"
-      "  --transport auto|local|tcp|rccl          inter-rank transport  [auto]\n"
+      "  --transport auto|local|tcp|rccl|loopback inter-rank transport  [auto]\n"
       "  --port P                rendezvous port (default MASTER_PORT+1 or 29600)\n"
-      "  --gpus N                one process, N GPU ranks as threads (loopback/peer copies;\n"
-      "                          with --transport rccl: one RCCL rank per GPU)\n"
+      "  --gpus N                one process, N GPU ranks as threads: RCCL (one rank per\n"
+      "                          GPU) when N GPUs are visible, else loopback D2D copies\n"
+      "  --watchdog S            multi-rank GPU runs: give up (abort the transport, exit 1)\n"
+      "                          after S s without device progress [300; 0 = never]\n"
       "  --phase-timing          per-phase times (exchange/compute/reduce) in --json; eager\n"
       "  --plan                  print the per-GPU memory plan (fields + halo buffers, worst\n"
       "                          rank, 288 GB HBM3E check) for --gpus/WORLD_SIZE ranks; exit\n"
@@ -291,6 +293,7 @@ int main(int argc, char** argv) {
     else if (a == "--checkpoint-every") o.ckpt_every = std::atoll(need().c_str());
     else if (a == "--resume") o.resume = need();
     else if (a == "--transport") transport = need();
+    else if (a == "--watchdog") setenv("HEAT_WATCHDOG_S", need().c_str(), 1);
     else if (a == "--port") port = std::atoi(need().c_str());
     else if (a == "--json") o.json = true;
     else if (a == "--gpus") gpus = std::atoi(need().c_str());
@@ -345,22 +348,29 @@ int main(int argc, char** argv) {
   if (P.backend == Backend::Hip) P.device = local_rank % ndev;
 
   if (gpus > 1 && world == 1) {
-    // One process, `gpus` ranks as threads over the loopback transport
-    // (peer copies between devices; ranks share devices round-robin when
-    // fewer GPUs are visible).
+    // One process, `gpus` ranks as threads, rank r on device r % ndev.  The
+    // transport follows heat::choose_group_transport (shared with
+    // parallel.group.run_group): RCCL -- one communicator rank per thread and
+    // GPU from one unique id, the ncclCommInitAll model of SURVEY R10,
+    // graph-captured exchanges -- whenever every rank has a GPU of its own;
+    // the loopback transport (D2D / peer copies) only for ranks sharing one.
     if (P.backend != Backend::Hip) {
       std::fprintf(stderr, "heat: --gpus needs the hip backend\n");
       return 2;
     }
-    // `--transport rccl`: one RCCL communicator rank per thread, one GPU
-    // each (the ncclCommInitAll process model of SURVEY R10; RCCL refuses two
-    // ranks on one device, so it needs `gpus` visible GPUs).
-    const bool rccl = transport == "rccl";
-    if (rccl && gpus > ndev) {
-      std::fprintf(stderr, "heat: --gpus %d --transport rccl needs %d GPUs, %d visible\n", gpus,
-                   gpus, ndev);
+    std::vector<int> devs(static_cast<size_t>(gpus));
+    for (int r = 0; r < gpus; ++r) devs[size_t(r)] = r % ndev;
+    GroupTransport kind;
+    try {
+      kind = choose_group_transport(transport == "auto" ? "auto" : transport, gpus, devs.data());
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "heat: --gpus %d: %s (%d GPUs visible)\n", gpus, e.what(), ndev);
       return 2;
     }
+    const bool rccl = kind == GroupTransport::Rccl;
+    if (std::getenv("HEAT_VERBOSE"))
+      std::fprintf(stderr, "heat: %d ranks as threads on %d GPU(s), transport %s\n", gpus, ndev,
+                   group_transport_name(kind));
     unsigned char uid[128] = {0};
     LoopbackHub* hub = nullptr;
     if (rccl)
@@ -373,7 +383,7 @@ int main(int argc, char** argv) {
       threads.emplace_back([&, r] {
         try {
           Params Pr = P;
-          Pr.device = r % ndev;
+          Pr.device = devs[size_t(r)];
           // ncclCommInitRank blocks until every rank joined: each rank
           // initialises on its own thread, concurrently.
           run_rank(o, Pr,
@@ -385,8 +395,9 @@ int main(int argc, char** argv) {
             // Loopback peers blocked on this rank's messages throw in turn.
             loopback_hub_fail(hub);
           } else {
-            // RCCL peers would block forever in ncclGroupEnd / collectives
-            // waiting for this rank: report and end the process now.
+            // RCCL peers would block in ncclGroupEnd / collectives waiting
+            // for this rank: report and end the process now (a fresh failure
+            // exit; the driver reclaims the device queues).
             std::fprintf(stderr, "heat: rank %d error: %s\n", r, e.what());
             std::fflush(stderr);
             std::_Exit(1);
@@ -435,6 +446,11 @@ int main(int argc, char** argv) {
     run_rank(o, P, std::move(tr));
   } catch (const std::exception& e) {
     std::fprintf(stderr, "heat: error: %s\n", e.what());
+    std::fflush(stderr);
+    // A multi-rank failure (e.g. the watchdog aborted the communicator with
+    // work still queued behind a dead peer): leave without running
+    // destructors that would wait on that work.
+    if (world > 1) std::_Exit(1);
     return 1;
   }
   return 0;

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define HEAT_ABI_VERSION 3
+#define HEAT_ABI_VERSION 4
 
 typedef struct heat_params {
   int64_t nx, ny;
@@ -117,6 +117,18 @@ int heat_loopback_hub_create(int world, void** out);
 int heat_loopback_hub_destroy(void* hub);
 /* A rank of the hub failed: peers blocked in an exchange or collective throw. */
 int heat_loopback_hub_fail(void* hub);
+/* Transport of a single-process multi-rank run (ranks = threads, rank r on
+   devices[r]): requested "auto" | "rccl" | "loopback"; *kind = 1 (rccl: every
+   rank has a GPU of its own) or 4 (loopback: ranks share a device).  The rule
+   of heat::choose_group_transport, shared by `heat --gpus N` and
+   parallel.group.run_group. */
+int heat_group_transport(const char* requested, int world, const int32_t* devices, int32_t* kind);
+/* Give up this rank: abort its transport (ncclCommAbort) so peers stop
+   waiting; a wait of the solver on another thread throws.  Thread-safe. */
+int heat_solver_abort(heat_solver* s);
+/* 1 if the automatic TB variant at `depth` takes a residual at any inner step
+   (checks ride inside full-depth passes), else 0. */
+int heat_tb_mid_residual(int depth);
 int heat_solver_reset(heat_solver* s);
 int heat_solver_info(heat_solver* s, heat_block_info* out);
 int heat_solver_step(heat_solver* s, int64_t* out);
@@ -159,16 +171,17 @@ int heat_op_tb_stamps(void* buf, int64_t waves);
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes /* nbox*4 */,
                     int nbox, int depth, unsigned* resid, void* stream, int waves_target,
-                    int variant /* -1 default; heat::gpu::tbv flags */);
+                    int variant /* -1 default; heat::gpu::tbv flags */,
+                    int res_level /* residual step 1..depth, 0 = depth */);
 /* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares;
    tile_rows / tile_waves: rows per wave / waves per workgroup of tile launches
-   (0 = planner). */
+   (0 = planner); tile_xl: tile lane shifts 0 DPP, 1 ds_bpermute, 2 mixed (-1 = default). */
 typedef struct heat_tb_tuning {
   int32_t variant, rounds, min_len, waves;
   double edge_frac;
   int32_t n_weights, tile_rows;
   double weights[4];
-  int32_t tile_waves, pad_;
+  int32_t tile_waves, tile_xl;
 } heat_tb_tuning;
 int heat_tb_get_tuning(heat_tb_tuning* out);
 int heat_tb_set_tuning(const heat_tb_tuning* in);

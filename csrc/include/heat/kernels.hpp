@@ -122,8 +122,15 @@ void lds_step(const float* src, float* dst, const StencilGeom& g, const Box& box
 void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                unsigned* resid, hipStream_t st);
 
+// res_level (with resid): the step 1..depth whose max |new - old| is taken;
+// 0 = depth (the pass's last step).  Inner levels need tb_mid_residual(depth).
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1);
+             int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1,
+             int res_level = 0);
+// The automatic variant choice at this depth takes a residual at any inner
+// level (depth 12: level-split pipelines or workgroup tiles), so a
+// convergence check can ride inside a full-depth pass instead of cutting it.
+bool tb_mid_residual(int depth);
 // Variant a launch of `depth` uses by default (HEAT_TB_VARIANT overrides).
 int tb_default_variant(int depth);
 // Variant tb_step picks for a launch of `depth` with this much work
@@ -154,6 +161,8 @@ struct TbTuning {
   std::vector<double> age_weights;
   int tile_rows = 0;       // HEAT_TB_TILE_ROWS: rows per wave of kTile launches (0: planner)
   int tile_waves = 0;      // HEAT_TB_TILE_WAVES: waves per kTile workgroup, 8 or 16 (0: planner)
+  int tile_xl = -1;        // HEAT_TB_TILE_XL: kTile lane shifts, 0 DPP, 1 ds_bpermute,
+                           // 2 mixed (-1: mixed unless the variant has kTileDpp)
 };
 TbTuning tb_tuning();  // a copy of the current set
 void tb_set_tuning(const TbTuning& t);

@@ -109,13 +109,19 @@ class Solver {
   void read_bin(const std::string& path);
   void synchronize();
   void barrier() { tr_->barrier(); }
+  // Gives up: aborts the transport (ncclCommAbort) so that this rank and its
+  // peers stop waiting on each other; a wait of this solver in progress (on
+  // another thread) throws, and the solver is unusable afterwards.  Used by
+  // a failing rank of a single-process group and by the watchdog.
+  void abort();
   // Device pointer (GPU) or host pointer (CPU) of owned cell (0,0) of the
   // buffer holding the current state.
   float* current() { return field_[cur_]; }
 
  private:
-  // One pass of a segment: k steps; rl = k: the pass ends at a check (its
-  // last level carries the residual), 0: no check.
+  // One pass of a segment: k steps; rl in 1..k: a check after the pass's
+  // rl-th step (its residual is taken at that level; rl = k: the pass ends at
+  // the check), 0: no check.
   struct PassPlan {
     int k = 0;
     int rl = 0;
@@ -139,6 +145,8 @@ class Solver {
   // Passes for steps [step0, step0+n), cut at every check point (the
   // residual is the last level of its pass).
   std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;
+  // A check may ride inside a depth-k pass (residual at an inner step).
+  bool mid_residual_ok(int k) const;
   void enqueue_segment(const std::vector<PassPlan>& plan);
   void enqueue_pass(int k, int rl);
   void exchange(int buf, int k, hipStream_t st);
@@ -148,6 +156,11 @@ class Solver {
   void compute_cpu(int k, int rl, int64_t er, int64_t ec);
   std::pair<int64_t, int64_t> ensure_ghosts(int k, hipStream_t st);
   float finish_resid();
+  // Device waits of the run loop: plain syncs on one rank; with peers, a
+  // polling wait with transport error checks and a no-progress timeout
+  // (HEAT_WATCHDOG_S, default 300 s, 0 = none), see wait_event.
+  void wait_event(hipEvent_t e);
+  void sync_watch();
   bool is_check_point(int64_t completed) const;
   int64_t next_check_after(int64_t step) const;
   bool converged_value(float r) const;
@@ -157,6 +170,9 @@ class Solver {
   bool gated() const { return on_gpu() && P_.converge && !staged_ && !host_checks_; }
   void run_segments(int64_t steps, RunStats& s);
   void run_gated(int64_t steps, RunStats& s);
+  // State of a converging check that sits inside pass p: its first p.rl
+  // steps again from the pass's source buffer.
+  void replay_check(const PassRec& p);
   // Launch (capturing on first use) the graph or the eager enqueue of one
   // segment; returns its pass records and check steps relative to step_.
   void launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_t phase,
@@ -175,6 +191,9 @@ class Solver {
   bool staged_ = false;  // GPU fields but host-memory transport
   bool host_checks_ = false;
   bool warmed_ = false;    // RCCL connections established outside capture
+  bool watch_ = false;     // multi-rank GPU run: waits poll with a watchdog
+  double watchdog_s_ = 300.0;
+  std::atomic<bool> aborted_{false};
   int64_t gr_ = 0, gc_ = 0;  // ghost rows/columns of field_[cur_] at the current level
   bool comm_pending_ = false;  // comm stream has unjoined work
   int cur_ = 0;
@@ -196,7 +215,7 @@ class Solver {
 
   // GPU state.
   hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
-  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr;
+  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_wait_ = nullptr;
   unsigned* d_resid_ = nullptr;
   float* h_resid_ = nullptr;
   void* d_scratch_ = nullptr;

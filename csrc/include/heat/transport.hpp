@@ -135,4 +135,22 @@ struct heat_callbacks {
 }
 std::unique_ptr<Transport> make_callback_transport(const heat_callbacks& cb);
 
+// Failure injection for tests: with HEAT_TEST_FAIL_AFTER=N in the
+// environment, the rank HEAT_TEST_FAIL_RANK (default 1) gets a wrapper that
+// throws from its (N+1)-th sendrecv / all-reduce; every other rank (and every
+// run without the variable) gets `tr` back unchanged.
+std::shared_ptr<Transport> maybe_inject_faults(std::shared_ptr<Transport> tr);
+
+// Transport of a single-process multi-rank run (`heat --gpus N`,
+// parallel.group.run_group): ranks are host threads, rank r on devices[r].
+// "auto": RCCL whenever every rank has a GPU of its own -- one communicator
+// rank per thread from one unique id, the ncclCommInitAll process model of
+// SURVEY R10 (mpi/mpi_heat_improved_persistent_stat.c:48-69 is what it
+// replaces), hipGraph-capturable -- and the loopback transport (D2D / peer
+// copies) only when ranks share a device, which RCCL refuses.  "rccl" /
+// "loopback" force one (rccl on shared devices throws).
+enum class GroupTransport : int { Rccl = 1, Loopback = 4 };
+GroupTransport choose_group_transport(const std::string& requested, int world, const int* devices);
+const char* group_transport_name(GroupTransport t);
+
 }  // namespace heat

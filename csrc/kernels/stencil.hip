@@ -275,6 +275,7 @@ TbTuning tuning_from_env() {
   t.waves = std::max(0, geti("HEAT_TB_WAVES", 0));
   t.tile_rows = std::max(0, geti("HEAT_TB_TILE_ROWS", 0));
   t.tile_waves = std::max(0, geti("HEAT_TB_TILE_WAVES", 0));
+  t.tile_xl = geti("HEAT_TB_TILE_XL", -1);
   if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);
   if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
     for (const char* q = e; *q;) {
@@ -452,10 +453,22 @@ void tb_set_stamps(unsigned long long* buf, int64_t waves) {
   else g_stamps.erase(dev);
 }
 
+bool tb_mid_residual(int depth) {
+  // Depth 12 under the automatic variant choice is always the level-split
+  // pipelines (tb_split_rl*.hip) or the workgroup tiles (tb_tile.hip), which
+  // take a residual at any inner step; forced variants keep the last step.
+  return depth == kTbDeepDepth && tb_tuning().variant < 0;
+}
+
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
-             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant) {
+             int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
+             int res_level) {
   HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
+  HEAT_CHECK(res_level >= 0 && res_level <= depth, "residual level %d of a depth-%d pass",
+             res_level, depth);
+  if (res_level == depth || resid == nullptr) res_level = 0;  // 0: the last step
+  const bool forced = variant >= 0 || tb_tuning().variant >= 0;
   const TbTuning tune = tb_tuning();
   if (variant < 0) {
     // Both defaults use float4 lanes (same strip width).
@@ -469,11 +482,15 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     // The tile kernel runs steps in (down, up) pairs: even depths only; an
     // odd pass (a remainder or a check-cut pass) streams.
     if (depth % 2 == 0) {
-      tbw::step(src, dst, g, boxes, nbox, depth, resid, st, variant, tune);
+      tbw::step(src, dst, g, boxes, nbox, depth, resid, res_level, st, variant, tune);
       return;
     }
     variant &= ~(tbv::kTile | tbv::kTileDpp);
   }
+  // Inner-level residuals: the level-split build at depth 12 (and the tiles).
+  HEAT_CHECK(res_level == 0 || (tb_variant_split(variant) && depth == kTbDeepDepth),
+             "a residual at step %d of a depth-%d pass needs the depth-12 level-split or tile "
+             "kernel (variant %d%s)", res_level, depth, variant, forced ? ", forced" : "");
   const int lag = tb_variant_lag(variant);
   const int W = tb_strip_width(depth, tb_lane_cols(variant));
   int64_t total_strip_rows = 0;
@@ -538,6 +555,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
   args.src = src;
   args.dst = dst;
   args.resid = resid;
+  args.res_level = res_level > 0 ? res_level : depth;
   args.g = g;
   args.flags = ((variant & tbv::kXcdGroups) ? tbdetail::kTbXcdGroups : 0) |
                ((variant & tbv::kAltDirection) ? tbdetail::kTbAltDirection : 0) |

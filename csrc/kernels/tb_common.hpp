@@ -27,6 +27,11 @@ struct TbArgs {
   StencilGeom g;
   int nbox, total_waves;
   int flags;  // kTbXcdGroups | kTbAltDirection | kTbAgePairs ...
+  // Residual level of a check pass (with resid != null): the step, 1..depth,
+  // whose max |new - old| is taken.  depth (or 0) = the pass's last step; a
+  // smaller level lets a check ride inside a full-depth pass instead of
+  // cutting it (tb_step's res_level; tile and level-split kernels).
+  int res_level;
   // kTbAgePairs: the grid is age_groups equal parts (dispatch rounds); a
   // group of age_groups vertically adjacent chunks is split between one unit
   // of each part at the cumulative row fractions age_cum[a] / 1024.
@@ -91,8 +96,8 @@ __device__ __forceinline__ void wave_max_atomic(unsigned m, unsigned* resid) {
 
 // The same with ONE global atomic per workgroup: every contributing wave
 // folds its max into an LDS word wg[0] and counts itself in wg[1]; the last
-// of the nact contributors (LDS requests of a wave execute in order, so all
-// earlier folds are in) publishes.  Per-wave atomics on the one residual word
+// of the nact contributors (the count's acquire-release orders all earlier
+// folds before it) publishes.  Per-wave atomics on the one residual word
 // from thousands of waves serialise at the memory side (~7 ns each: ~37 us
 // per check pass at 4000 waves).  No barrier: waves of the block may have
 // exited already.  wg must be zeroed (and a barrier passed) at kernel start.
@@ -100,10 +105,13 @@ __device__ __forceinline__ void group_max_atomic(unsigned m, unsigned* resid, un
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = max(m, unsigned(__shfl_xor(int(m), off)));
   if ((threadIdx.x & 63) == 0) {
+    // Release / acquire at workgroup scope: the memory model (not just the
+    // in-order LDS queue of one wave) orders every contributor's max before
+    // its count, and the last contributor's count before its read of the max.
     __hip_atomic_fetch_max(wg, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned n = __hip_atomic_fetch_add(wg + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned n = __hip_atomic_fetch_add(wg + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (int(n) == nact - 1)
-      atomicMax(resid, __hip_atomic_load(wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      atomicMax(resid, __hip_atomic_load(wg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
   }
 }
 
@@ -120,6 +128,11 @@ int occupancy(int depth, int lag);
 namespace heat::gpu::tbx {  // level-split two-wave pipelines (tb_split.hip)
 bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);
 int occupancy_split(int depth);
+// Depth-12 launches with the residual at inner level rl (tb_split_rl{a,b,c}.hip:
+// levels 1-4, 5-8, 9-11); false if rl is not in the unit's range.
+bool launch_split_rl_a(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
+bool launch_split_rl_b(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
+bool launch_split_rl_c(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 }
 namespace heat::gpu::tbn {  // float2 lanes (tb_narrow.hip)
 bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);

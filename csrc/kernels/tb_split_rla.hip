@@ -1,0 +1,15 @@
+// Inner-level residual kernels of the level-split build (depth 12, residual
+// levels 1..4): a convergence check that falls inside a full-depth pass takes
+// its residual at that level instead of cutting the pass (tb_stream.inl,
+// TbStream RS; solver plan_passes).  One unit per range of levels so the
+// instantiations compile in parallel; same flags as tb_split.hip.
+#include "tb_common.hpp"
+
+#define HEAT_TB_NS tbx
+#define HEAT_TB_PACKED 0
+#define HEAT_TB_SPLIT 1
+#define HEAT_TB_BPERMUTE 1
+#define HEAT_TB_SPLIT_RL_LO 1
+#define HEAT_TB_SPLIT_RL_HI 4
+#define HEAT_TB_SPLIT_RL_FN launch_split_rl_a
+#include "tb_stream.inl"

@@ -163,15 +163,23 @@ __device__ constexpr int modn(int v) {
   return ((v % N) + N) % N;
 }
 
-// RES: this launch computes the fused residual (check passes only); the
-// other passes get an instantiation without the |delta| max per element.
+// RS: the level (1..K) whose residual max |new - old| this launch takes (a
+// check pass), 0 = none; the other passes get an instantiation without it.
+// RS = K (not stage 0) is taken at emit time, next to the store; an inner
+// level (or stage 0's last, which goes to the LDS ring) right after the
+// level's update, over the unit's output rows [qrb, qrb + qlen): a check
+// that falls inside a full-depth pass rides on it instead of cutting the
+// pass (LAG 3 pipelines).
 // ROLE (the level-split pipeline, tb_split.hip): 0 = the whole pipeline;
 // 1 = stage 0, levels 1..K of a two-wave pipeline, emitting its last level
 // into the LDS ring of the pair (all lanes, rows [rb, re) of the stage);
 // 2 = stage 1, reading its input rows from that ring instead of memory.
-template <int K, int LAG, int MODE, bool RES, int ROLE = 0>
+template <int K, int LAG, int MODE, int RS, int ROLE = 0>
 struct TbStream {
   static constexpr bool ROWCHK = MODE == kModeGeneric;
+  static constexpr bool LASTRES = RS == K && ROLE != 1;
+  static constexpr bool MIDRES = RS > 0 && !LASTRES;
+  static_assert(!MIDRES || LAG == 3, "inner-level residuals need the LAG 3 pipeline");
   // LAG 3 = LAG 1 pipeline with the compile-time ramp (see run()).
   static constexpr int RING = LAG == 0 ? 2 : (LAG == 2 ? 4 : 3);
   // Prefetch distance in rows (LAG 3: part of the 6-row level-0 ring L0).
@@ -183,6 +191,7 @@ struct TbStream {
   vecf L0[LAG == 3 ? 6 : 1];  // LAG 3: level-0 rows t-2 .. t+3 (see lv())
   float m = 0.f;  // residual max |delta| (RES)
   int rc = V;  // elements of this lane inside the box (the residual skips the rest)
+  int qrb = 0, qlen = 0;  // MIDRES: the unit's output rows (local, 32-bit)
   // src / dst (run() arguments) point at the strip's first column, the same
   // for every lane (scalar registers); lane l adds lo = V * l elements, so
   // loads and stores use the scalar-base + 32-bit lane-offset addressing
@@ -260,7 +269,7 @@ struct TbStream {
     }
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
-      if constexpr (RES) {
+      if constexpr (LASTRES) {
         // max |delta| with the NaN-propagating IEEE-2019 maximum
         // (v_maximum3_f32, abs folded into its inputs): a NaN or inf
         // anywhere reaches the judge.  Columns past the box end (the last
@@ -273,6 +282,20 @@ struct TbStream {
         for (int j = 0; j < V; j += 2)
           m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(d[j], d[j + 1]));
       }
+    }
+  }
+
+  // MIDRES: fold max |nw - old| of level-RS row `row` (uniform) into m if
+  // the row is one of the unit's output rows (this lane's stored columns).
+  __device__ __forceinline__ void acc_mid(const vecf& nw, const vecf& old, int64_t row,
+                                          bool store_lane) {
+    if (unsigned(int(row) - qrb) < unsigned(qlen) && store_lane) {
+      float d[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] = (j == 0 || rc > j) ? __builtin_fabsf(nw[j] - old[j]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < V; j += 2)
+        m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(d[j], d[j + 1]));
     }
   }
 
@@ -374,36 +397,42 @@ struct TbStream {
       const bool ok = !ROWCHK || row_in(i - s, rlo, rhi);
       lv(s, T6 - s) = HEAT_TB_UPD(s, lv(s - 1, T6 - s - 1), lv(s - 1, T6 - s),
                                   lv(s - 1, T6 - s + 1), ok);
+      if constexpr (MIDRES && RS < K) {
+        if (s == RS) acc_mid(lv(s, T6 - s), lv(s - 1, T6 - s), i - s, store_lane);
+      }
     }
     const int64_t ro = i - K;  // output row of this iteration
     const bool ok = !ROWCHK || row_in(ro, rlo, rhi);
     const vecf& b = lv(K - 1, T6 - K);
     const vecf out = HEAT_TB_UPD(K, lv(K - 1, T6 - K - 1), b, lv(K - 1, T6 - K + 1), ok);
+    if constexpr (MIDRES && RS == K) acc_mid(out, b, ro, store_lane);
 #undef HEAT_TB_UPD
     emit<FAST>(out, b, ro, dst, pitch, rb, re, store_lane, woff);
   }
 
   template <int T, int S>
-  __device__ __forceinline__ void ramp_levels(int64_t i, int rlo, int rhi,
+  __device__ __forceinline__ void ramp_levels(int64_t i, int rlo, int rhi, bool store_lane,
                                               const RowUpdate<MODE>& upd) {
     if constexpr (S < K) {
       if constexpr (2 * S <= T) {
         const bool ok = !ROWCHK || row_in(i - S, rlo, rhi);
         lv(S, T - S) = upd(lv(S - 1, T - S - 1), lv(S - 1, T - S), lv(S - 1, T - S + 1), ok);
+        // Ramp rows of an inner level can be output rows (t >= K + S).
+        if constexpr (MIDRES && S == RS) acc_mid(lv(S, T - S), lv(S - 1, T - S), i - S, store_lane);
       }
-      ramp_levels<T, S + 1>(i, rlo, rhi, upd);
+      ramp_levels<T, S + 1>(i, rlo, rhi, store_lane, upd);
     }
   }
   template <int T>
   __device__ __forceinline__ void ramp(int64_t first_in, const float* __restrict__ src,
                                        int64_t pitch, int64_t last_in, int rlo, int rhi,
-                                       const RowUpdate<MODE>& upd) {
+                                       bool store_lane, const RowUpdate<MODE>& upd) {
     if constexpr (T < 2 * K) {
       const int64_t i = first_in + T;
       L0[modn<6>(T + 3)] = load_row(src, min(i + 3, last_in), pitch);
-      ramp_levels<T, 1>(i, rlo, rhi, upd);
+      ramp_levels<T, 1>(i, rlo, rhi, store_lane, upd);
       __builtin_amdgcn_sched_barrier(0);
-      ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, upd);
+      ramp<T + 1>(first_in, src, pitch, last_in, rlo, rhi, store_lane, upd);
     }
   }
 
@@ -429,7 +458,7 @@ struct TbStream {
       // 2s useless rows per level per chunk (a third of all work for short
       // chunks).  The ramp is unrolled at compile time, one scheduling
       // region per iteration (keeps register pressure at the loop's level).
-      ramp<0>(first_in, src, pitch, last_in, rlo, rhi, upd);
+      ramp<0>(first_in, src, pitch, last_in, rlo, rhi, store_lane, upd);
       constexpr int T0 = 2 * K;
       int64_t t = T0;
       // Main-loop groups t .. t+5 with t + 5 + 3 <= last_in - first_in
@@ -530,8 +559,11 @@ __device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, 
 // levels 1..K1 (into the LDS ring), stage 1 levels K1+1..K (`ring`, `cnt`:
 // the pair's LDS ring and its two counters; `qoff`: ring sequence number of
 // the segment's first row, so consecutive segments of one unit keep the
-// ring protocol's numbers monotonic).  Returns this lane's residual max.
-template <int K, int LAG, int K1>
+// ring protocol's numbers monotonic).  RLM > 0: a check pass whose residual
+// is taken at pipeline level RLM < K (stage 0 if RLM <= K1); only the
+// interior and generic Dirichlet modes are built for it (edge strips take
+// the generic path).  Returns this lane's residual max.
+template <int K, int LAG, int K1, int RLM = 0>
 __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, int strip,
                                                int chunk, int64_t rb, int64_t re, int stage,
                                                vecf* ring, unsigned* cnt, int64_t qoff) {
@@ -590,18 +622,28 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
     } else if constexpr (MD >= 2) {
       upd.cm[0] = gy <= g.ny - 1 && g.ny - 1 < gy + V;  // this lane holds column ny-1
     }
+    constexpr bool RES = decltype(res_c)::value;
+    // Residual level of each stream (0 = none), see TbStream RS.
+    constexpr int RS_ALL = RLM > 0 ? RLM : (RES ? K : 0);
+    constexpr int RS_ST0 = (RLM > 0 && RLM <= K1) ? RLM : 0;
+    constexpr int RS_ST1 = RLM > K1 ? RLM - K1 : ((RLM == 0 && RES) ? K2 : 0);
     if constexpr (K1 == 0) {
-      TbStream<K, LAG, MD, decltype(res_c)::value> st;
+      TbStream<K, LAG, MD, RS_ALL> st;
       st.lo = V * lane;
       st.rc = int(min<int64_t>(cend - col, V));
+      st.qrb = int(rb);
+      st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     } else if (stage == 0) {
       // Level-K1 rows [rb - K2, re + K2): exactly what stage 1's trapezoid reads.
-      TbStream<K1, LAG, MD, false, 1> st;
+      TbStream<K1, LAG, MD, RS_ST0, 1> st;
       st.lo = V * lane;
+      st.rc = int(min<int64_t>(cend - col, V));
+      st.qrb = int(rb);
+      st.qlen = int(re - rb);
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
@@ -610,22 +652,29 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
     } else {
-      TbStream<K2, LAG, MD, decltype(res_c)::value, 2> st;
+      TbStream<K2, LAG, MD, RS_ST1, 2> st;
       st.lo = V * lane;
       st.ring = ring;
       st.produced = cnt;
       st.released = cnt + 1;
       st.qoff = qoff;
       st.rc = int(min<int64_t>(cend - col, V));
+      st.qrb = int(rb);
+      st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     }
   };
   auto go = [&](auto mode_c) {
-    if (want_resid) go2(mode_c, std::true_type{});
-    else go2(mode_c, std::false_type{});
+    if (RLM > 0 || !want_resid) go2(mode_c, std::false_type{});
+    else go2(mode_c, std::true_type{});
   };
+  if constexpr (RLM > 0) {
+    if (mode == 0) go(std::integral_constant<int, 0>{});
+    else go(std::integral_constant<int, kModeGeneric>{});
+    return m;
+  }
   switch (mode) {
     case 0: go(std::integral_constant<int, 0>{}); break;
     case 1: go(std::integral_constant<int, 1>{}); break;
@@ -663,7 +712,7 @@ __device__ __forceinline__ int64_t tb_lin_boundary(const TbArgs& a, int64_t x) {
 // group of G chunks split between G units).  Linear plans: a range of the
 // strip-row sequence, run as consecutive segments (a strip end, a box end
 // or a row where the Dirichlet mode changes starts a new segment).
-template <int K, int LAG, int K1>
+template <int K, int LAG, int K1, int RLM = 0>
 __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
                                        unsigned* cnt, unsigned* wg, int nact) {
   constexpr int K2 = K - K1;
@@ -707,7 +756,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
       re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
     }
-    if (rb < re) m = tb_segment<K, LAG, K1>(a, bx, strip, chunk, rb, re, stage, ring, cnt, 0);
+    if (rb < re) m = tb_segment<K, LAG, K1, RLM>(a, bx, strip, chunk, rb, re, stage, ring, cnt, 0);
   } else {
     // Linear plan: as many segments as the unit's range crosses.
     int64_t qoff = 0;
@@ -729,11 +778,13 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
       else if (rb < bot && re > bot) re = bot;
       x0 += re - rb;
       m = __builtin_elementwise_maximum(
-          m, tb_segment<K, LAG, K1>(a, bx, strip, chunk, rb, re, stage, ring, cnt, qoff));
+          m, tb_segment<K, LAG, K1, RLM>(a, bx, strip, chunk, rb, re, stage, ring, cnt, qoff));
       qoff += (re - rb) + 2 * K2;
     }
   }
-  if (a.resid != nullptr && (K1 == 0 || stage == 1))
+  // One contributor per pipeline: the wave whose levels hold the residual.
+  constexpr int res_stage = (RLM > 0 && RLM <= K1) ? 0 : 1;
+  if (a.resid != nullptr && (K1 == 0 || stage == res_stage))
     tbdetail::group_max_atomic(__float_as_uint(m), a.resid, wg, nact);
   if (a.stamps && lane == 0) {
     const int64_t idx = int64_t(wave) + int64_t(age) * a.total_waves;
@@ -777,7 +828,7 @@ template <int K, int K1>
 constexpr int tb_split_waves_per_simd() {
   return tb_waves_per_simd<(K1 > K - K1 ? K1 : K - K1), 3>();
 }
-template <int K, int K1>
+template <int K, int K1, int RLM = 0>
 __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_split_kernel(TbArgs a) {
   __shared__ vecf ring[2][kSplitRing * 64];
   __shared__ unsigned cnt[2][2];
@@ -797,7 +848,7 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_sp
     nact += tb_unit(a, 2, q, ag) < a.total_waves ? 1 : 0;
   }
   if (unit >= a.total_waves) return;
-  tb_run<K, 3, K1>(a, unit, age, wid & 1, ring[p], cnt[p], wg, nact);
+  tb_run<K, 3, K1, RLM>(a, unit, age, wid & 1, ring[p], cnt[p], wg, nact);
 }
 #endif
 
@@ -828,6 +879,7 @@ int occ_k() {
   return std::max(1, n);
 }
 
+#if !HEAT_TB_SPLIT_RL_LO  // the residual-level units define only their launcher
 // Resident 256-thread blocks per CU of the (depth, lag) instantiation.
 int occupancy(int depth, int lag) {
 #if HEAT_TB_DEEP
@@ -903,13 +955,37 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
   }
 }
 
+#endif  // !HEAT_TB_SPLIT_RL_LO
+
 #if HEAT_TB_SPLIT
-template <int K, int K1>
+template <int K, int K1, int RLM = 0>
 void launch_split_k(const TbArgs& args, hipStream_t st) {
   int blocks = int((args.total_waves + 1) / 2);  // two pipelines per block
   if (args.flags & tbdetail::kTbAgePairs) blocks = (blocks + 7) / 8 * 8 * args.age_groups;
-  hipLaunchKernelGGL((tb_split_kernel<K, K1>), dim3(blocks), dim3(256), 0, st, args);
+  hipLaunchKernelGGL((tb_split_kernel<K, K1, RLM>), dim3(blocks), dim3(256), 0, st, args);
 }
+#endif
+#if HEAT_TB_SPLIT_RL_LO
+// A build unit of inner-level residual kernels (depth 12, levels LO..HI):
+// the eleven instantiations are spread over three units that compile in
+// parallel (tb_split_rl{a,b,c}.hip).
+template <int RL>
+bool launch_split_rl_range(const TbArgs& args, int rl, hipStream_t st) {
+  if constexpr (RL > HEAT_TB_SPLIT_RL_HI) {
+    return false;
+  } else {
+    if (rl == RL) {
+      launch_split_k<12, 6, RL>(args, st);
+      return true;
+    }
+    return launch_split_rl_range<RL + 1>(args, rl, st);
+  }
+}
+bool HEAT_TB_SPLIT_RL_FN(const TbArgs& args, int depth, int rl, hipStream_t st) {
+  return depth == 12 && launch_split_rl_range<HEAT_TB_SPLIT_RL_LO>(args, rl, st);
+}
+#endif
+#if HEAT_TB_SPLIT && !HEAT_TB_SPLIT_RL_LO
 template <int K, int K1>
 int occ_split_k() {
   int n = 0;
@@ -928,6 +1004,10 @@ int occ_split_k() {
 // Tcells/s at 8192^2, bench 3.83 / 3.80 vs 5.17 (3 waves per SIMD,
 // profiles/r3_raw/r3ab3_*.log).
 bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
+  const int rl = args.res_level;
+  if (args.resid != nullptr && rl > 0 && rl < depth)  // a check inside the pass
+    return launch_split_rl_a(args, depth, rl, st) || launch_split_rl_b(args, depth, rl, st) ||
+           launch_split_rl_c(args, depth, rl, st);
   switch (depth) {
     case 8: launch_split_k<8, 4>(args, st); return true;
     case 12: launch_split_k<12, 6>(args, st); return true;

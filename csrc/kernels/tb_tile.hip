@@ -130,7 +130,9 @@ struct Upd {
   }
 };
 
-template <int R, int MODE, bool RES, int XL>
+// RES: 0 no residual, 1 residual on the last step (with the stores), 2 on
+// an inner step (TbArgs::res_level, a check inside a full-depth pass).
+template <int R, int MODE, int RES, int XL>
 struct Tile {
   vecf u[R];
   float m = 0.f;
@@ -144,10 +146,11 @@ struct Tile {
   // lets the register allocator put new row r where old row r -/+ 1 was (dead
   // by then) and be back at the loop's assignment after two steps: one
   // direction only needed a copy of every row per step at the back-edge.
-  // LAST: the launch's last step stores every useful row as soon as it is
-  // computed (dst + off0 + r * pitch, this lane's columns if store_lane) and,
-  // with RES, accumulates max |new - old| over the useful cells.
-  template <bool DOWN, bool LAST, class Xc>
+  // WHAT 1 (LAST): the launch's last step stores every useful row as soon as
+  // it is computed (dst + off0 + r * pitch, this lane's columns if
+  // store_lane) and, with RES 1, accumulates max |new - old| over the useful
+  // cells; WHAT 2: an inner step that only accumulates the residual (RES 2).
+  template <bool DOWN, int WHAT, class Xc>
   __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, XL>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
                                        float* __restrict__ dst, int64_t off0, int64_t pitch) {
@@ -182,11 +185,13 @@ struct Tile {
       u[r] = up.apply(n, cur, so, wl[r], er[r], (rowmask >> r) & 1u);
       if (i == 0) xc.publish(0, u[r]);
       if (i == R - 1) xc.publish(1, u[r]);
-      if constexpr (LAST) {
+      if constexpr (WHAT == 1) {
         if ((usemask >> r) & 1u) {
           if (store_lane) *reinterpret_cast<vecf*>(dst + off0 + r * pitch) = u[r];
-          if constexpr (RES) acc(u[r], cur, store_lane, rc);
+          if constexpr (RES == 1) acc(u[r], cur, store_lane, rc);
         }
+      } else if constexpr (WHAT == 2) {
+        if ((usemask >> r) & 1u) acc(u[r], cur, store_lane, rc);
       }
       prev = cur;
       if (i == R / 2 - 1) last_nb = xc.mid();
@@ -207,7 +212,7 @@ struct Tile {
   }
 };
 
-template <int R, int NW, int MODE, bool RES, int XL>
+template <int R, int NW, int MODE, int RES, int XL>
 __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int strip, int t, int K,
                                           vecf (*xch)[2][NW][64]) {
   const int lane = threadIdx.x & 63;
@@ -304,15 +309,31 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   };
   using Down = std::true_type;
   using Up = std::false_type;
+  using Plain = std::integral_constant<int, 0>;
+  using Last = std::integral_constant<int, 1>;
+  using Mid = std::integral_constant<int, 2>;
   // Steps in (down, up) pairs (K is even, see launch()); the residual rides
-  // on the last up step.
+  // on the last up step (RES 1) or on step res_level - 1 (RES 2: a uniform
+  // branch per step picks the body that accumulates it).
   int s = 0;
-  for (; s + 2 < K; s += 2) {
-    xstep(Down{}, std::false_type{}, s);
-    xstep(Up{}, std::false_type{}, s + 1);
+  if constexpr (RES == 2) {
+    const int rs = a.res_level - 1;
+    for (; s + 2 < K; s += 2) {
+      if (s == rs) xstep(Down{}, Mid{}, s);
+      else xstep(Down{}, Plain{}, s);
+      if (s + 1 == rs) xstep(Up{}, Mid{}, s + 1);
+      else xstep(Up{}, Plain{}, s + 1);
+    }
+    if (s == rs) xstep(Down{}, Mid{}, s);
+    else xstep(Down{}, Plain{}, s);
+  } else {
+    for (; s + 2 < K; s += 2) {
+      xstep(Down{}, Plain{}, s);
+      xstep(Up{}, Plain{}, s + 1);
+    }
+    xstep(Down{}, Plain{}, s);
   }
-  xstep(Down{}, std::false_type{}, s);
-  xstep(Up{}, std::true_type{}, s + 1);
+  xstep(Up{}, Last{}, s + 1);
   return T.m;
 }
 
@@ -350,12 +371,16 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
   const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
   float m;
+  // Residual: none, on the last step, or on an inner step (res_level).
+  const int res = a.resid == nullptr ? 0 : (a.res_level > 0 && a.res_level < K) ? 2 : 1;
   if (interior) {
-    m = a.resid ? tile_run<R, NW, 0, true, XL>(a, bx, strip, t, K, xch)
-                : tile_run<R, NW, 0, false, XL>(a, bx, strip, t, K, xch);
+    m = res == 0 ? tile_run<R, NW, 0, 0, XL>(a, bx, strip, t, K, xch)
+        : res == 1 ? tile_run<R, NW, 0, 1, XL>(a, bx, strip, t, K, xch)
+                   : tile_run<R, NW, 0, 2, XL>(a, bx, strip, t, K, xch);
   } else {
-    m = a.resid ? tile_run<R, NW, 1, true, XL>(a, bx, strip, t, K, xch)
-                : tile_run<R, NW, 1, false, XL>(a, bx, strip, t, K, xch);
+    m = res == 0 ? tile_run<R, NW, 1, 0, XL>(a, bx, strip, t, K, xch)
+        : res == 1 ? tile_run<R, NW, 1, 1, XL>(a, bx, strip, t, K, xch)
+                   : tile_run<R, NW, 1, 2, XL>(a, bx, strip, t, K, xch);
   }
   if (a.resid != nullptr) {
     // One atomic per workgroup: a per-wave atomicMax on the one residual
@@ -468,7 +493,7 @@ int cached_occupancy(int rows, int waves, int bp) {
 // stall together at its barriers; calibrated on the 8-GPU blocks,
 // profiles/r3_tile.md).
 void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox, int depth,
-          unsigned* resid, hipStream_t st, int variant, const TbTuning& tune) {
+          unsigned* resid, int res_level, hipStream_t st, int variant, const TbTuning& tune) {
   struct Shape {
     int rows, waves;
   };
@@ -476,12 +501,9 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
   // Lane shifts: mixed (2: the left shift a DPP wave shift folded into the
   // add, the right one ds_bpermute issued ahead; +3-6 % over ds_bpermute for
   // both, which waited on LDS issue 13 % of the time, profiles/r3_tile.md)
-  // unless the variant asks for DPP (0); HEAT_TB_TILE_XL=0/1/2 overrides.
-  static const int xl_env = [] {
-    const char* e = std::getenv("HEAT_TB_TILE_XL");
-    return e && *e ? std::atoi(e) : -1;
-  }();
-  const int bp = xl_env >= 0 && xl_env <= 2 ? xl_env : (variant & tbv::kTileDpp) ? 0 : 2;
+  // unless the variant asks for DPP (0); TbTuning::tile_xl (HEAT_TB_TILE_XL)
+  // 0/1/2 overrides.
+  const int bp = tune.tile_xl >= 0 && tune.tile_xl <= 2 ? tune.tile_xl : (variant & tbv::kTileDpp) ? 0 : 2;
   const int W = tb_strip_width(depth, 4);
   const int cus = tb_simd_count() / 4;
   Shape best{0, 0};
@@ -511,6 +533,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
   args.src = src;
   args.dst = dst;
   args.resid = resid;
+  args.res_level = res_level > 0 && res_level < depth ? res_level : depth;
   args.g = g;
   args.flags = (variant & tbv::kXcdGroups) ? tbdetail::kTbXcdGroups : 0;
   int n = 0;

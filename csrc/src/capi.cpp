@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "heat/common.hpp"
 #include "heat/cpu_backend.hpp"
@@ -443,14 +444,15 @@ int heat_op_mfma_step(const float* src, float* dst, int64_t pitch, int64_t gx0, 
 
 int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, int64_t gy0,
                     int64_t nx, int64_t ny, float cx, float cy, const int64_t* boxes, int nbox,
-                    int depth, unsigned* resid, void* stream, int waves_target, int variant) {
+                    int depth, unsigned* resid, void* stream, int waves_target, int variant,
+                    int res_level) {
   return guard([&] {
     HEAT_CHECK(nbox >= 1 && nbox <= 5, "nbox %d", nbox);
     heat::Box b[5];
     for (int i = 0; i < nbox; ++i)
       b[i] = heat::Box{boxes[4 * i], boxes[4 * i + 1], boxes[4 * i + 2], boxes[4 * i + 3]};
     heat::gpu::tb_step(src, dst, geom(pitch, gx0, gy0, nx, ny, cx, cy), b, nbox, depth, resid,
-                       S(stream), waves_target, variant);
+                       S(stream), waves_target, variant, res_level);
   });
 }
 
@@ -465,6 +467,7 @@ int heat_tb_get_tuning(heat_tb_tuning* out) {
     out->edge_frac = t.edge_frac;
     out->tile_rows = t.tile_rows;
     out->tile_waves = t.tile_waves;
+    out->tile_xl = t.tile_xl;
     out->n_weights = int32_t(std::min<size_t>(t.age_weights.size(), 4));
     for (int i = 0; i < out->n_weights; ++i) out->weights[i] = t.age_weights[size_t(i)];
   });
@@ -482,6 +485,7 @@ int heat_tb_set_tuning(const heat_tb_tuning* in) {
     t.edge_frac = in->edge_frac;
     t.tile_rows = std::max(0, in->tile_rows);
     t.tile_waves = std::max(0, in->tile_waves);
+    t.tile_xl = in->tile_xl;
     t.age_weights.assign(in->weights, in->weights + in->n_weights);
     heat::gpu::tb_set_tuning(t);
   });
@@ -529,5 +533,22 @@ int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows,
 }
 
 int heat_tb_supported(int depth) { return heat::gpu::tb_depth_supported(depth) ? 1 : 0; }
+
+int heat_tb_mid_residual(int depth) { return heat::gpu::tb_mid_residual(depth) ? 1 : 0; }
+
+int heat_group_transport(const char* requested, int world, const int32_t* devices, int32_t* kind) {
+  return guard([&] {
+    HEAT_CHECK(world >= 1 && devices != nullptr && kind != nullptr, "heat_group_transport: bad args");
+    std::vector<int> d(devices, devices + world);
+    *kind = int32_t(heat::choose_group_transport(requested ? requested : "auto", world, d.data()));
+  });
+}
+
+int heat_solver_abort(heat_solver* s) {
+  return guard([&] {
+    HEAT_CHECK(s && s->s, "null solver");
+    s->s->abort();
+  });
+}
 
 }  // extern "C"

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "heat/common.hpp"
 #include "heat/cpu_backend.hpp"
@@ -37,7 +38,8 @@ void host_unpack(const float* buf, float* origin, int64_t pitch, const Box& b) {
 
 }  // namespace
 
-Solver::Solver(const Params& p, std::shared_ptr<Transport> tr) : P_(p), tr_(std::move(tr)) {
+Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
+    : P_(p), tr_(maybe_inject_faults(std::move(tr))) {
   HEAT_CHECK(tr_ != nullptr, "no transport");
   HEAT_CHECK(P_.nx >= 1 && P_.ny >= 1, "grid %lldx%lld", (long long)P_.nx, (long long)P_.ny);
   HEAT_CHECK(P_.check_interval >= 1, "check interval %d", P_.check_interval);
@@ -100,6 +102,10 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr) : P_(p), tr_(std:
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
   host_checks_ = env_int("HEAT_HOST_CHECKS", 0) != 0;
   timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
+  // Waits on the device poll the transport and give up after this long
+  // without completion (multi-rank GPU runs; wait_event).
+  watch_ = on_gpu() && world > 1;
+  if (const char* w = std::getenv("HEAT_WATCHDOG_S"); w && *w) watchdog_s_ = std::atof(w);
   try {
     alloc();
     init_fields();
@@ -134,6 +140,7 @@ void Solver::alloc() {
     }
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&d_resid_, 256));
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
@@ -171,6 +178,12 @@ void Solver::alloc() {
 }
 
 void Solver::free_all() {
+  if (on_gpu() && aborted_) {
+    // The transport was aborted with work still queued that may never
+    // complete (it waits for a dead peer): leave the device memory and
+    // streams to process teardown rather than block here.
+    return;
+  }
   if (on_gpu()) {
     if (s_comp_) (void)hipStreamSynchronize(s_comp_);
     if (s_comm_) (void)hipStreamSynchronize(s_comm_);
@@ -193,7 +206,7 @@ void Solver::free_all() {
     if (d_checksum_) (void)hipFree(d_checksum_);
     if (d_gate_) (void)hipFree(d_gate_);
     if (h_gate_) (void)hipHostFree(h_gate_);
-    for (auto e : {ev_ready_, ev_halo_, ev_seg_[0], ev_seg_[1]})
+    for (auto e : {ev_ready_, ev_halo_, ev_wait_, ev_seg_[0], ev_seg_[1]})
       if (e) (void)hipEventDestroy(e);
     for (auto e : event_pool_) (void)hipEventDestroy(e);
     event_pool_.clear();
@@ -212,7 +225,7 @@ void Solver::free_all() {
   h_resid_ = nullptr;
   d_scratch_ = d_checksum_ = nullptr;
   d_gate_ = h_gate_ = nullptr;
-  ev_ready_ = ev_halo_ = ev_seg_[0] = ev_seg_[1] = nullptr;
+  ev_ready_ = ev_halo_ = ev_wait_ = ev_seg_[0] = ev_seg_[1] = nullptr;
   s_comp_ = s_comm_ = nullptr;
 }
 
@@ -305,30 +318,54 @@ std::vector<int> Solver::pass_depths(int64_t n) const {
   return d;
 }
 
+bool Solver::mid_residual_ok(int k) const {
+  // A check inside a pass needs (a) one launch per pass reading a source
+  // buffer nothing else writes during the pass (so a converging check can be
+  // replayed from it, replay_check) and (b) a kernel that takes the residual
+  // at any step: depth-12 TB passes under the automatic variant choice.
+  return gated() && tb_kernel() && gpu::tb_mid_residual(k);
+}
+
 std::vector<Solver::PassPlan> Solver::plan_passes(int64_t step0, int64_t n) const {
-  // Segments end at check points, so every check is the last step of a pass
-  // and the kernel takes its residual at the pass's last level (emit time).
-  // A residual at an arbitrary inner level (one uniform branch per level and
-  // row) measured +33 % (split pipelines) / +57 % (single wave) per check
-  // pass at 8192^2 against +12 % / +1 % at the last level
-  // (profiles/r3_residual_cost.md): cutting passes at checks is cheaper.
+  // Full-depth passes whatever the check phase: a check that falls inside a
+  // pass takes its residual at that step (rl < k) of the pass's launch, so
+  // checks cost a residual, not a cut pass (was: every check ended a pass,
+  // 50 steps = 12,12,12,7,7; 8192^2 checking every 20 steps -12 %,
+  // profiles/r3_residual_cost.md).  Where that is not possible (kernels
+  // without inner-level residuals, or two checks inside one pass) the pass is
+  // cut at the check as before and the rest re-planned.
+  // Reference: the check every STEP steps, mpi/...c:235-262,
+  // cuda/cuda_heat.cu:219-236.
   std::vector<PassPlan> out;
   int64_t pos = step0;
   const int64_t end = step0 + n;
+  std::vector<int> d = pass_depths(n);
+  size_t i = 0;
   while (pos < end) {
-    int64_t seg = end - pos;
-    bool check = false;
-    if (P_.converge) {
-      const int64_t c = next_check_after(pos);
-      if (c <= end) {
-        seg = c - pos;
-        check = true;
-      }
+    HEAT_CHECK(i < d.size(), "pass plan ran out at step %lld of %lld", (long long)pos,
+               (long long)end);
+    const int k = d[i];
+    int64_t c = P_.converge ? next_check_after(pos) : INT64_MAX;
+    if (c > pos + k) {  // no check in this pass
+      out.push_back({k, 0});
+      pos += k;
+      ++i;
+      continue;
     }
-    const auto d = pass_depths(seg);
-    for (size_t i = 0; i < d.size(); ++i)
-      out.push_back({d[i], check && i + 1 == d.size() ? d[i] : 0});
-    pos += seg;
+    const bool one = next_check_after(c) > pos + k;
+    if (one && (c == pos + k || mid_residual_ok(k))) {
+      out.push_back({k, int(c - pos)});
+      pos += k;
+      ++i;
+      continue;
+    }
+    // Cut at the check, then plan the rest anew.
+    const auto cut = pass_depths(c - pos);
+    for (size_t j = 0; j < cut.size(); ++j)
+      out.push_back({cut[j], j + 1 == cut.size() ? cut[j] : 0});
+    pos = c;
+    d = pass_depths(end - pos);
+    i = 0;
   }
   return out;
 }
@@ -510,7 +547,7 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
   }
 
   if (!split) {
-    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, &own, 1, k, r, st, waves_target, -1, rl);
     return;
   }
   // Boundary bands are `band` >= k deep (k for exchange-first; H for the
@@ -522,10 +559,10 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
   const int64_t c1 = nb[East] >= 0 ? round_down(ly - band, 4) : ly;
   if (part == 0) {
     Box in{r0, r1, c0, c1};
-    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, &in, 1, k, r, st, waves_target, -1, rl);
   } else {
     Box b[4] = {{0, r0, 0, ly}, {r1, lx, 0, ly}, {r0, r1, 0, c0}, {r0, r1, c1, ly}};
-    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target);
+    gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target, -1, rl);
     // cur_ flips once per pass, after the boundary part.
   }
 }
@@ -723,7 +760,7 @@ float Solver::finish_resid() {
   TraceRange trace("heat.residual_wait");
   float r;
   if (on_gpu()) {
-    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    sync_watch();
     check_staged();
     tr_->check();
     std::memcpy(&r, h_resid_, 4);
@@ -951,13 +988,13 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
                              hipMemcpyDeviceToHost, s_comp_));
     HIP_CHECK(hipEventRecord(ev_seg_[j & 1], s_comp_));
     if (j >= 1) {
-      HIP_CHECK(hipEventSynchronize(ev_seg_[(j - 1) & 1]));
+      wait_event(ev_seg_[(j - 1) & 1]);
       stopped = gate_h[(j - 1) & 1].stop != 0;
     }
     remaining -= seg;
     ++j;
   }
-  synchronize();
+  sync_watch();
   const gpu::DeviceGate gate = gate_h[(j - 1) & 1];
   s.checks = gate.checks;
   if (gate.checks > 0) std::memcpy(&s.last_resid, &gate.last_bits, 4);
@@ -968,23 +1005,46 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   HEAT_CHECK(gate.stop_check < all_checks.size(), "gate closed at check %u of %zu",
              gate.stop_check, all_checks.size());
   const int64_t c = all_checks[gate.stop_check];
+  const PassRec* p = nullptr;
+  for (const auto& r : all_recs)
+    if (r.rl > 0 && r.step0 + r.rl == c) p = &r;
+  HEAT_CHECK(p != nullptr, "no pass takes the residual of check step %lld", (long long)c);
+  // Passes behind the closing check wrote nothing: the state of that check
+  // is the output of its pass, or, for a check inside a pass, the pass's
+  // first rl steps replayed from its (untouched) source buffer.  Restored
+  // before a non-finite residual is reported too, so gather() / save() after
+  // the error see the check's state, as on the host-judged path.
+  if (p->rl == p->k) {
+    cur_ = p->cur1;
+    gr_ = p->gr1;
+    gc_ = p->gc1;
+  } else {
+    replay_check(*p);
+  }
+  step_ = c;
+  s.steps_done = c - step0;
   if (gate.reason == 2)
     throw_error(__FILE__, __LINE__,
                 strprintf("non-finite residual (%g) at step %lld", double(s.last_resid),
                           (long long)c));
-  const PassRec* p = nullptr;
-  for (const auto& r : all_recs)
-    if (r.step0 + r.k == c && r.rl == r.k) p = &r;
-  HEAT_CHECK(p != nullptr, "no pass ends at check step %lld", (long long)c);
-  // Passes behind the converging check wrote nothing: the state of that
-  // check is the output of its pass.
-  cur_ = p->cur1;
-  gr_ = p->gr1;
-  gc_ = p->gc1;
-  step_ = c;
-  s.steps_done = c - step0;
   s.converged = true;
   s.converged_at = c;
+}
+
+void Solver::replay_check(const PassRec& p) {
+  // The pass read field_[p.cur0] (owned block plus ghosts valid at least k
+  // deep, exchanged or computed before it) and wrote only the other buffer;
+  // every later launch was gated off, and later exchanges only re-sent those
+  // same frozen states.  Its first rl steps over the owned block alone need
+  // rl <= k ghost levels and no exchange: every rank replays locally.
+  TraceRange trace("heat.replay_check");
+  HEAT_CHECK(tb_kernel(), "replay of an inner-pass check needs the TB kernel");
+  HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(unsigned), s_comp_));  // reopen: DeviceGate::stop
+  cur_ = p.cur0;
+  compute_gpu(p.rl, 0, false, 0);
+  cur_ ^= 1;
+  gr_ = gc_ = 0;  // the replayed buffer's ghosts are stale
+  sync_watch();
 }
 
 RunStats Solver::run(int64_t steps) {
@@ -1006,14 +1066,14 @@ RunStats Solver::run(int64_t steps) {
     // exchange of the current buffer is idempotent.
     exchange(cur_, H_, s_comp_);
     tr_->allreduce_max(reinterpret_cast<float*>(d_scratch_), 1, s_comp_);
-    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    sync_watch();
     warmed_ = true;
   }
   if (steps > 0) {
     if (gated()) run_gated(steps, s);
     else run_segments(steps, s);
   }
-  synchronize();
+  sync_watch();
   check_staged();
   tr_->check();
   s.seconds = now_s() - t0;
@@ -1027,6 +1087,67 @@ RunStats Solver::run(int64_t steps) {
   s.passes = stat_passes_ - p0;
   s.exchanges = stat_exchanges_ - e0;
   return s;
+}
+
+void Solver::wait_event(hipEvent_t e) {
+  // The reference's ranks block in MPI_Waitall / MPI_Allreduce
+  // (mpi/mpi_heat_improved_persistent_stat.c:177, :255) and hang with a dead
+  // peer.  Here a multi-rank GPU wait polls: it spins on hipEventQuery for a
+  // few thousand tries (the common case: a segment that is about to end),
+  // then sleeps between polls, asks the transport for asynchronous errors
+  // every 50 ms (ncclCommGetAsyncError) and gives up after watchdog_s_
+  // seconds without completion.  Either way the transport is aborted
+  // (ncclCommAbort) and the call throws: a fresh failure exit, no retry.
+  if (!watch_) {
+    HIP_CHECK(hipEventSynchronize(e));
+    return;
+  }
+  const double t0 = now_s();
+  double next_poll = t0 + 0.05;
+  for (int spin = 0;; ++spin) {
+    if (aborted_.load())
+      throw_error(__FILE__, __LINE__, strprintf("rank %d: run aborted", tr_->rank()));
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIP_CHECK(q);
+    if (spin < 4096) {
+      std::this_thread::yield();
+      continue;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    const double t = now_s();
+    if (t < next_poll) continue;
+    next_poll = t + 0.05;
+    try {
+      check_staged();
+      tr_->check();
+    } catch (...) {
+      abort();
+      throw;
+    }
+    if (watchdog_s_ > 0 && t - t0 > watchdog_s_) {
+      abort();
+      throw_error(__FILE__, __LINE__,
+                  strprintf("rank %d: no progress on the device for %.0f s (HEAT_WATCHDOG_S): a "
+                            "peer rank died or hung; transport aborted",
+                            tr_->rank(), watchdog_s_));
+    }
+  }
+}
+
+void Solver::sync_watch() {
+  if (!watch_) {
+    synchronize();
+    return;
+  }
+  HIP_CHECK(hipEventRecord(ev_wait_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_wait_, 0));
+  HIP_CHECK(hipEventRecord(ev_wait_, s_comp_));
+  wait_event(ev_wait_);
+}
+
+void Solver::abort() {
+  if (!aborted_.exchange(true)) tr_->abort();
 }
 
 void Solver::synchronize() {

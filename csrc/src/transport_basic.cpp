@@ -1,5 +1,9 @@
-// Local (world of one) and callback transports.
+// Local (world of one) and callback transports, the fault-injection
+// wrapper used by the failure-detection tests, and the transport choice of
+// single-process multi-rank runs.
+#include <cstdlib>
 #include <cstring>
+#include <set>
 
 #include "heat/common.hpp"
 #include "heat/transport.hpp"
@@ -58,7 +62,87 @@ class CallbackTransport final : public Transport {
   heat_callbacks cb_;
 };
 
+// Forwards to `inner` and throws from the (after+1)-th message or collective
+// call: a rank that dies mid-run (HEAT_TEST_FAIL_AFTER, see
+// maybe_inject_faults).  Its peers then wait for messages that never come;
+// what they must do is fail within their watchdog instead of hanging
+// (Solver::wait_event; the reference's MPI_Allreduce, mpi/...c:255, would
+// block forever).
+class FaultTransport final : public Transport {
+ public:
+  FaultTransport(std::shared_ptr<Transport> inner, int64_t after)
+      : in_(std::move(inner)), left_(after) {}
+  int rank() const override { return in_->rank(); }
+  int world() const override { return in_->world(); }
+  bool device_memory() const override { return in_->device_memory(); }
+  bool graph_capturable() const override { return in_->graph_capturable(); }
+  void sendrecv(const Msg* msgs, int n, hipStream_t st) override {
+    tick("sendrecv");
+    in_->sendrecv(msgs, n, st);
+  }
+  void allreduce_max(float* buf, int count, hipStream_t st) override {
+    tick("allreduce_max");
+    in_->allreduce_max(buf, count, st);
+  }
+  void allreduce_sum_f64(double* buf, int count, hipStream_t st) override {
+    tick("allreduce_sum_f64");
+    in_->allreduce_sum_f64(buf, count, st);
+  }
+  void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) override {
+    tick("allreduce_sum_u64");
+    in_->allreduce_sum_u64(buf, count, st);
+  }
+  void barrier() override { in_->barrier(); }
+  void check() override { in_->check(); }
+  void abort() override { in_->abort(); }
+  const char* name() const override { return in_->name(); }
+  TransportInfo info() const override { return in_->info(); }
+
+ private:
+  void tick(const char* what) {
+    if (left_-- <= 0)
+      throw_error(__FILE__, __LINE__,
+                  strprintf("injected transport failure on rank %d at %s (HEAT_TEST_FAIL_AFTER)",
+                            in_->rank(), what));
+  }
+  std::shared_ptr<Transport> in_;
+  int64_t left_;
+};
+
 }  // namespace
+
+std::shared_ptr<Transport> maybe_inject_faults(std::shared_ptr<Transport> tr) {
+  const char* after = std::getenv("HEAT_TEST_FAIL_AFTER");
+  if (!after || !*after || !tr) return tr;
+  const char* rk = std::getenv("HEAT_TEST_FAIL_RANK");
+  const int rank = rk && *rk ? std::atoi(rk) : 1;
+  if (tr->rank() != rank) return tr;
+  return std::make_shared<FaultTransport>(std::move(tr), std::atoll(after));
+}
+
+GroupTransport choose_group_transport(const std::string& requested, int world,
+                                      const int* devices) {
+  HEAT_CHECK(world >= 1 && devices != nullptr, "choose_group_transport: world %d", world);
+  std::set<int> seen;
+  bool own = true;  // every rank has a device of its own
+  for (int r = 0; r < world; ++r) {
+    HEAT_CHECK(devices[r] >= 0, "rank %d has no device (%d)", r, devices[r]);
+    own = seen.insert(devices[r]).second && own;
+  }
+  if (requested == "loopback") return GroupTransport::Loopback;
+  if (requested == "rccl") {
+    HEAT_CHECK(own, "transport rccl needs one GPU per rank (RCCL refuses two ranks on one "
+               "device); %d ranks share %zu device(s)", world, seen.size());
+    return GroupTransport::Rccl;
+  }
+  HEAT_CHECK(requested == "auto" || requested.empty(),
+             "unknown group transport '%s' (auto, rccl, loopback)", requested.c_str());
+  return own && world > 1 ? GroupTransport::Rccl : GroupTransport::Loopback;
+}
+
+const char* group_transport_name(GroupTransport t) {
+  return t == GroupTransport::Rccl ? "rccl" : "loopback";
+}
 
 std::unique_ptr<Transport> make_local_transport() { return std::make_unique<LocalTransport>(); }
 

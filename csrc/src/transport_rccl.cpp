@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "heat/common.hpp"
@@ -39,6 +40,7 @@ class RcclTransport final : public Transport {
   }
   ~RcclTransport() override {
     if (scratch_) (void)hipFree(scratch_);
+    std::lock_guard<std::mutex> lk(mu_);
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   int rank() const override { return rank_; }
@@ -46,8 +48,12 @@ class RcclTransport final : public Transport {
   bool device_memory() const override { return true; }
   bool graph_capturable() const override { return true; }
 
+  // Every call holds mu_: abort() may come from another thread (a failing
+  // rank of a single-process group, or a solver's watchdog) and frees comm_.
   void sendrecv(const Msg* msgs, int n, hipStream_t st) override {
     if (n == 0) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < n; ++i) {
       const Msg& m = msgs[i];
@@ -57,12 +63,18 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max(float* buf, int count, hipStream_t st) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat, ncclMax, comm_, st));
   }
   void allreduce_sum_f64(double* buf, int count, hipStream_t st) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat64, ncclSum, comm_, st));
   }
   void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclUint64, ncclSum, comm_, st));
   }
   void barrier() override {
@@ -70,19 +82,34 @@ class RcclTransport final : public Transport {
     // A one-element all-reduce on a private stream, then wait for it.
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclFloat, ncclMax, comm_, st));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      live();
+      NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclFloat, ncclMax, comm_, st));
+    }
     HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipStreamDestroy(st));
   }
   void check() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     ncclResult_t async = ncclSuccess;
     NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
     if (async != ncclSuccess && async != ncclInProgress)
       throw_error(__FILE__, __LINE__,
                   std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
   }
+  // ncclCommAbort: RCCL's kernels and proxy threads stop waiting for peers
+  // that will never answer; later calls throw.  Idempotent.
+  void abort() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
   const char* name() const override { return "rccl"; }
   TransportInfo info() const override {
+    std::lock_guard<std::mutex> lk(mu_);
+    live();
     TransportInfo t;
     NCCL_CHECK(ncclCommCount(comm_, &t.nranks));
     NCCL_CHECK(ncclCommCuDevice(comm_, &t.device));
@@ -93,7 +120,11 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  void live() const {
+    if (!comm_) throw_error(__FILE__, __LINE__, "RCCL communicator was aborted");
+  }
   int rank_, world_;
+  mutable std::mutex mu_;
   ncclComm_t comm_ = nullptr;
   float* scratch_ = nullptr;
 };

@@ -22,7 +22,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be imported before libheat: shared HIP runtime)
 
-ABI_VERSION = 3  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
+ABI_VERSION = 4  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
@@ -107,7 +107,7 @@ class HeatTbTuning(Structure):
     _fields_ = [("variant", c_int32), ("rounds", c_int32), ("min_len", c_int32),
                 ("waves", c_int32), ("edge_frac", c_double), ("n_weights", c_int32),
                 ("tile_rows", c_int32), ("weights", c_double * 4), ("tile_waves", c_int32),
-                ("pad_", c_int32)]
+                ("tile_xl", c_int32)]
 
 
 class HeatChecksum(Structure):
@@ -164,7 +164,7 @@ _SIGS = {
                                   c_void_p, c_void_p]),
     "heat_op_tb_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                 c_float, c_float, POINTER(c_int64), c_int, c_int, c_void_p,
-                                c_void_p, c_int, c_int]),
+                                c_void_p, c_int, c_int, c_int]),
     "heat_tb_get_tuning": (c_int, [POINTER(HeatTbTuning)]),
     "heat_tb_set_tuning": (c_int, [POINTER(HeatTbTuning)]),
     "heat_op_tb_stamps": (c_int, [c_void_p, c_int64]),
@@ -179,6 +179,9 @@ _SIGS = {
     "heat_layout": (c_int, [c_int64, c_int64, c_int, POINTER(c_int64), POINTER(c_int64),
                             POINTER(c_int), POINTER(c_int)]),
     "heat_tb_supported": (c_int, [c_int]),
+    "heat_tb_mid_residual": (c_int, [c_int]),
+    "heat_group_transport": (c_int, [ctypes.c_char_p, c_int, POINTER(c_int32), POINTER(c_int32)]),
+    "heat_solver_abort": (c_int, [c_void_p]),
 }
 
 

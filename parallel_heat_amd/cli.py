@@ -59,9 +59,15 @@ def build_parser() -> argparse.ArgumentParser:
     a("--halo-passes", type=int, default=0)
     a("--numerics", choices=["fp32", "mpi"], default="fp32")
     a("--phase-timing", action="store_true")
-    a("--transport", choices=["auto", "local", "rccl", "torch", "tcp"], default="auto")
+    a("--transport", choices=["auto", "local", "rccl", "torch", "tcp", "loopback"], default="auto",
+      help="loopback: --gpus ranks sharing a device (native binary)")
     a("--port", type=int, default=0, help="tcp transport rendezvous port (0: MASTER_PORT+1)")
-    a("--gpus", type=int, default=0, help="one process, N GPU ranks as threads (native binary)")
+    a("--gpus", type=int, default=0,
+      help="one process, N GPU ranks as threads (native binary): RCCL with a GPU per rank, "
+           "else loopback copies")
+    a("--watchdog", type=float, default=None,
+      help="multi-rank GPU runs: abort and exit 1 after this many seconds without device "
+           "progress (HEAT_WATCHDOG_S, default 300, 0 = never)")
     a("--plan", action="store_true", help="print the per-GPU memory plan and exit (native)")
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
@@ -77,6 +83,11 @@ def main(argv=None) -> int:
         # Single-process native modes: the `heat` binary owns the threads
         # and the planner; same flags, same output.
         return subprocess.run([str(_native.CLI_PATH)] + argv).returncode
+    if args.watchdog is not None:
+        import os
+        os.environ["HEAT_WATCHDOG_S"] = str(args.watchdog)  # read by the native solver
+    if args.transport == "loopback":
+        raise SystemExit("--transport loopback is the --gpus mode of ranks sharing a device")
     backend = args.backend or ("hip" if torch.cuda.is_available() else "cpu")
     compat = args.compat or {"mpi": "mpi", "cuda": "cuda"}.get(args.naming, "none")
     cfg = HeatConfig(nx=args.nx, ny=args.ny, steps=args.steps, cx=args.cx, cy=args.cy,

@@ -84,9 +84,11 @@ class HeatSolver:
     def __init__(self, config: HeatConfig, transport: str = "auto",
                  dist_info: Optional[pcomm.DistInfo] = None, device: Optional[int] = None,
                  hub: Optional[pcomm.LoopbackHub] = None, group=None,
-                 shared: Optional[pcomm.EngineTransport] = None):
+                 shared: Optional[pcomm.EngineTransport] = None,
+                 rccl_uid: Optional[bytes] = None):
         """`shared`: an existing EngineTransport (e.g. the run's one RCCL
-        communicator) instead of building a new transport."""
+        communicator) instead of building a new transport.  `rccl_uid`: the
+        RCCL unique id shared by ranks that are threads of one process."""
         self.config = config
         config.validate()
         if config.backend == "hip":
@@ -119,13 +121,20 @@ class HeatSolver:
                          ctypes.byref(h))
         else:
             self._comm, self._keep = pcomm.make_comm(transport, self.dist, device=max(device, 0),
-                                                     hub=hub, group=group)
+                                                     hub=hub, group=group, rccl_uid=rccl_uid)
             _native.call("heat_solver_create", ctypes.byref(params), ctypes.byref(self._comm),
                          ctypes.byref(h))
         self._h = h
         self.info = self._info()
 
     # -- lifecycle -----------------------------------------------------------
+    def abort(self) -> None:
+        """Give up this rank: abort its transport (ncclCommAbort) so that its
+        peers stop waiting for it; a wait of this solver on another thread
+        raises.  Thread-safe; the solver is unusable afterwards."""
+        if getattr(self, "_h", None):
+            _native.call("heat_solver_abort", self._h)
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             _native.call("heat_solver_destroy", self._h)

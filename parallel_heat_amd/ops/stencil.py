@@ -62,13 +62,15 @@ class TbTuning:
     age_weights: List[float] = field(default_factory=list)
     tile_rows: int = 0  # rows per wave of TILE launches (0: planner)
     tile_waves: int = 0  # waves per TILE workgroup, 8 or 16 (0: planner)
+    tile_xl: int = -1  # TILE lane shifts: 0 DPP, 1 ds_bpermute, 2 mixed (-1: default)
 
 
 def tb_tuning() -> TbTuning:
     t = _native.HeatTbTuning()
     _native.call("heat_tb_get_tuning", ctypes.byref(t))
     return TbTuning(t.variant, t.rounds, t.min_len, t.waves, t.edge_frac,
-                    [t.weights[i] for i in range(t.n_weights)], t.tile_rows, t.tile_waves)
+                    [t.weights[i] for i in range(t.n_weights)], t.tile_rows, t.tile_waves,
+                    t.tile_xl)
 
 
 def set_tb_tuning(t: TbTuning) -> None:
@@ -77,7 +79,8 @@ def set_tb_tuning(t: TbTuning) -> None:
         raise ValueError("at most 4 age weights")
     c = _native.HeatTbTuning(int(t.variant), int(t.rounds), int(t.min_len), int(t.waves),
                              float(t.edge_frac), n, int(t.tile_rows),
-                             (ctypes.c_double * 4)(*t.age_weights), int(t.tile_waves), 0)
+                             (ctypes.c_double * 4)(*t.age_weights), int(t.tile_waves),
+                             int(t.tile_xl))
     _native.call("heat_tb_set_tuning", ctypes.byref(c))
 
 
@@ -208,11 +211,13 @@ def mfma_step(src: Field, dst: Field, geom: Geom, box: Optional[Box] = None,
 
 def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
             boxes: Optional[Sequence[Box]] = None, resid: Optional[torch.Tensor] = None,
-            waves_target: int = 0, variant: int = -1) -> None:
+            waves_target: int = 0, variant: int = -1, res_level: int = 0) -> None:
     """`depth` fused Jacobi steps (temporally blocked kernel) over up to 5 boxes.
 
     variant: -1 = chosen per launch (TbVariant.DEFAULT, or DEFAULT_DEEP for
-    large depth-12 launches); otherwise TbVariant flags.
+    large depth-12 launches); otherwise TbVariant flags.  res_level (with
+    resid): the step 1..depth whose max |new - old| goes to resid (0 = the
+    last; inner levels need tb_mid_residual(depth)).
     """
     if src.device.type == "cpu":
         raise ValueError("tb_step is a GPU kernel")
@@ -226,7 +231,7 @@ def tb_step(src: Field, dst: Field, geom: Geom, depth: int,
     _native.call("heat_op_tb_step", ctypes.c_void_p(src.ptr()), ctypes.c_void_p(dst.ptr()),
                  src.pitch, geom.gx0, geom.gy0, geom.nx, geom.ny, geom.cx, geom.cy, arr,
                  len(boxes), depth, ctypes.c_void_p(rp) if rp else None,
-                 ctypes.c_void_p(_stream()), waves_target, int(variant))
+                 ctypes.c_void_p(_stream()), waves_target, int(variant), int(res_level))
 
 
 def tb_stamps(buf: Optional[torch.Tensor]) -> None:

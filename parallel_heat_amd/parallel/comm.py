@@ -23,7 +23,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -143,6 +143,18 @@ class TorchDistTransport:
         comm.barrier = self._cb_barrier
 
 
+def group_transport(requested: str, devices: Sequence[int]) -> str:
+    """Transport of a single-process multi-rank run with rank r on devices[r]:
+    "rccl" when every rank has a GPU of its own, "loopback" when ranks share
+    one ("auto"); "rccl" / "loopback" force one.  The native rule
+    (heat::choose_group_transport) that `heat --gpus N` uses too."""
+    arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+    kind = ctypes.c_int32(0)
+    _native.call("heat_group_transport", requested.encode(), len(devices), arr,
+                 ctypes.byref(kind))
+    return {1: "rccl", 4: "loopback"}[kind.value]
+
+
 def broadcast_bytes(data: Optional[bytes], src: int = 0) -> bytes:
     """Broadcast a small byte string from `src` over the default process group."""
     obj = [data]
@@ -178,11 +190,15 @@ class LoopbackHub:
 
 
 def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = None,
-              port: Optional[int] = None, hub: Optional[LoopbackHub] = None, group=None):
+              port: Optional[int] = None, hub: Optional[LoopbackHub] = None, group=None,
+              rccl_uid: Optional[bytes] = None):
     """Build a native HeatComm (and the Python object that must outlive it).
 
     `group`: torch.distributed process group of the ``torch`` transport
-    (default: the default group; it must support CPU tensors, e.g. gloo)."""
+    (default: the default group; it must support CPU tensors, e.g. gloo).
+    `rccl_uid`: the RCCL unique id, when the ranks are threads of one process
+    that already share it (parallel.group.run_group); otherwise rank 0 makes
+    one and torch.distributed broadcasts it."""
     comm = _native.HeatComm()
     keep = None
     if kind == "loopback":
@@ -196,8 +212,11 @@ def make_comm(kind: str, info: DistInfo, device: int = 0, addr: Optional[str] = 
         comm.kind = 0
         comm.rank, comm.world = 0, 1
     elif kind == "rccl":
-        uid = _native.rccl_unique_id() if info.rank == 0 else None
-        uid = broadcast_bytes(uid)
+        if rccl_uid is not None:
+            uid = rccl_uid
+        else:
+            uid = _native.rccl_unique_id() if info.rank == 0 else None
+            uid = broadcast_bytes(uid)
         comm.kind = 1
         comm.rank, comm.world, comm.device = info.rank, info.world, device
         ctypes.memmove(comm.unique_id, uid, 128)

@@ -1,9 +1,16 @@
-"""Several ranks in one process: one host thread per rank over the loopback
-transport (device buffers, stream-ordered D2D / peer copies).
+"""Several ranks in one process: one host thread per rank.
 
-This is the single-process multi-GPU mode (ranks on devices 0..N-1) and the
-way the device-memory exchange path runs with real concurrency on ONE GPU,
-where RCCL refuses two ranks ("decomposition invariance (1 GPU)").
+This is the single-process multi-GPU mode (one process owning N
+GPUs, the reference's ``MPI_Init`` world of ``mpi/mpi_heat_improved_persistent_stat.c:48-69``)
+and the way the device-memory exchange path runs with real concurrency on ONE
+GPU.  The transport follows the native rule that ``heat --gpus N`` uses too
+(``heat::choose_group_transport``, ``parallel.comm.group_transport``):
+
+* every rank on a GPU of its own: **RCCL**, one communicator rank per thread
+  from one unique id (the ``ncclCommInitAll`` model), hipGraph-captured
+  exchanges;
+* ranks sharing a device: the **loopback** transport (device buffers,
+  stream-ordered D2D / peer copies), since RCCL refuses two ranks per device.
 
     results = run_group(HeatConfig(nx=8192, ny=8192, steps=1000), world=4,
                         fn=lambda s: (s.run(), s.gather()))
@@ -13,37 +20,72 @@ from __future__ import annotations
 import threading
 from typing import Callable, List, Optional, Sequence
 
+from .. import _native
 from ..models.config import HeatConfig
 from ..models.heat2d import HeatSolver
 from . import comm as pcomm
 
 
+def default_devices(config: HeatConfig, world: int) -> List[int]:
+    """Rank r's GPU: config.device for every rank if set, else r % visible GPUs."""
+    if config.device >= 0:
+        return [config.device] * world
+    n = max(1, _native.device_count())
+    return [r % n for r in range(world)]
+
+
 def run_group(config: HeatConfig, world: int, fn: Callable[[HeatSolver], object],
-              devices: Optional[Sequence[int]] = None) -> List[object]:
+              devices: Optional[Sequence[int]] = None,
+              transport: str = "auto") -> List[object]:
     """Run `fn(solver)` on `world` ranks (threads); returns the per-rank results.
 
-    `devices[r]` is rank r's GPU (default: all on device 0, or config.device).
+    `devices[r]` is rank r's GPU (default: default_devices).  `transport`:
+    "auto" (RCCL with a GPU per rank, else loopback), "rccl" or "loopback".
     Every rank must make the same sequence of collective calls (run, gather,
     checksum, ...), as with one process per rank."""
     if config.backend != "hip":
-        raise ValueError("the loopback transport needs backend='hip'")
-    hub = pcomm.LoopbackHub(world)
-    if devices is None:
-        devices = [max(config.device, 0)] * world
+        raise ValueError("single-process groups need backend='hip'")
+    devices = list(devices) if devices is not None else default_devices(config, world)
+    if len(devices) != world:
+        raise ValueError(f"{len(devices)} devices for {world} ranks")
+    kind = pcomm.group_transport(transport, devices)
+    hub = pcomm.LoopbackHub(world) if kind == "loopback" else None
+    uid = _native.rccl_unique_id() if kind == "rccl" else None
     results: List[object] = [None] * world
     errors: List[Optional[BaseException]] = [None] * world
+    solvers: List[Optional[HeatSolver]] = [None] * world
+    lock = threading.Lock()
+
+    def fail_peers(rank: int) -> None:
+        # Unblock the peers, which would wait forever for this rank's
+        # messages: loopback peers raise "a peer rank failed"; RCCL peers have
+        # their communicators aborted (their waits raise "run aborted").
+        if hub is not None:
+            hub.fail()
+            return
+        with lock:
+            peers = [s for r, s in enumerate(solvers) if s is not None and r != rank]
+        for s in peers:
+            try:
+                s.abort()
+            except Exception:  # noqa: BLE001 - best effort
+                pass
 
     def body(rank: int) -> None:
         try:
             info = pcomm.DistInfo(rank, world, rank)
-            with HeatSolver(config, transport="loopback", dist_info=info,
-                            device=devices[rank], hub=hub) as s:
-                results[rank] = fn(s)
+            with HeatSolver(config, transport=kind, dist_info=info, device=devices[rank],
+                            hub=hub, rccl_uid=uid) as s:
+                with lock:
+                    solvers[rank] = s
+                try:
+                    results[rank] = fn(s)
+                finally:
+                    with lock:
+                        solvers[rank] = None
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             errors[rank] = e
-            # Unblock the peers (they would wait forever for this rank's
-            # messages); they raise "a peer rank failed" in turn.
-            hub.fail()
+            fail_peers(rank)
 
     threads = [threading.Thread(target=body, args=(r,), name=f"heat-rank{r}")
                for r in range(world)]
@@ -51,11 +93,13 @@ def run_group(config: HeatConfig, world: int, fn: Callable[[HeatSolver], object]
         t.start()
     for t in threads:
         t.join()
-    hub.close()
-    # Report the first failure, not the peers' "a peer rank failed" echoes.
+    if hub is not None:
+        hub.close()
+    # Report the first failure, not the peers' echoes.
     failed = [(r, e) for r, e in enumerate(errors) if e is not None]
     if failed:
-        own = [(r, e) for r, e in failed if "a peer rank failed" not in str(e)]
+        echo = ("a peer rank failed", "run aborted", "communicator was aborted")
+        own = [(r, e) for r, e in failed if not any(x in str(e) for x in echo)]
         r, e = (own or failed)[0]
         raise RuntimeError(f"rank {r} failed: {e}") from e
     return results

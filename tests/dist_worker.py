@@ -58,7 +58,7 @@ def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
     cs = s.checksum()
     if rank == 0:
         np.savez(out_path, grid=g, conv=conv, conv_at=conv_at, done=done, hash=cs["hash"],
-                 px=s.info.px, py=s.info.py, exchanges=r.exchanges)
+                 px=s.info.px, py=s.info.py, exchanges=r.exchanges, schedule=s.info.schedule)
     s.close()
     dist.barrier()
     dist.destroy_process_group()

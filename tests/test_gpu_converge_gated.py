@@ -80,3 +80,27 @@ def test_gated_single_step_kernels(gpu, kernel):
     c, rc = _run(cfg.replace(backend="cpu", tb_depth=1))
     assert r.converged_at == rc.converged_at
     assert np.array_equal(g, c)
+
+
+@pytest.mark.parametrize("check", [2, 4])
+def test_gated_split_kernel_check_inside_pass(gpu, check):
+    # A plate large enough for the level-split pipelines (>= 64 strip-rows
+    # per SIMD at depth 12).  Checks every 20 steps no longer cut the 12-step
+    # passes: the check after step 40 is taken at level 4 of pass [36, 48),
+    # the one after step 80 at level 8 of pass [72, 84), the one after step 60
+    # at the end of pass [48, 60).  eps is set just above the CPU oracle's
+    # residual at the chosen check, so the run converges exactly there and
+    # its state is the inner-pass replay.
+    base = HeatConfig(nx=2048, ny=8192, steps=0, converge=True, check_interval=20, eps=0.0,
+                      init="random", seed=9, backend="cpu", tb_depth=1)
+    with HeatSolver(base) as c:
+        res = [np.float32(c.run(20).last_resid) for _ in range(check)]
+        want = c.gather()
+    assert all(res[i] > res[i + 1] for i in range(len(res) - 1)), res
+    eps = float(np.nextafter(res[-1], np.float32(np.inf)))
+    cfg = base.replace(backend="hip", tb_depth=12, eps=eps)
+    g, r = _run(cfg, 200)
+    assert r.converged and r.converged_at == 20 * check, (r.converged_at, res)
+    assert r.checks == check
+    assert np.float32(r.last_resid) == res[-1]
+    assert np.array_equal(g, want), np.abs(g - want).max()

@@ -156,6 +156,68 @@ def test_tb_residual(gpu, k, variant):
     assert ops.resid_value(resid) == float((last - prev).abs().max())
 
 
+def _cpu_levels(g, lx, ly, halo, k, seed, box=None):
+    """Owned-block states after 0..k naive steps on the CPU (box = slice of a
+    larger plate when the block is a subdomain)."""
+    a = ops.Field(lx, ly, halo, "cpu")
+    b = ops.Field(lx, ly, halo, "cpu")
+    ops.init_field(a, g, "random", seed)
+    ops.init_field(b, g, "random", seed)
+    out = [a.owned().clone()]
+    for _ in range(k):
+        ops.naive_step(a, b, g, (0, lx, 0, ly))
+        a, b = b, a
+        out.append(a.owned().clone())
+    if box is not None:
+        r0, r1, c0, c1 = box
+        out = [o[r0:r1, c0:c1] for o in out]
+    return out
+
+
+TILE = V.TILE | V.XCD_GROUPS
+
+
+@pytest.mark.parametrize("variant", [DEEP, DEEP | V.LINEAR, DEEP | V.ALT_DIRECTION,
+                                     DEEP | V.FORCE_AGE_PAIRS, TILE])
+@pytest.mark.parametrize("where", ["plate", "interior"])
+def test_tb_inner_level_residual(gpu, variant, where):
+    # A convergence check inside a full-depth pass: the launch takes the
+    # residual at step rl (1..12) and still writes the 12-step state.  Plate:
+    # every tile / strip touches the Dirichlet ring (generic masked path);
+    # interior: a block inside a larger plate (unmasked path).
+    k = 12
+    if where == "plate":
+        lx, ly, seed = 203, 517, 3
+        g, a, b = _fields(lx, ly, k, gpu, seed=seed)
+        levels = _cpu_levels(g, lx, ly, k, k, seed)
+    else:
+        NX, NY, seed = 260, 900, 5
+        ox, oy, lx, ly = 60, 256, 140, 520
+        g = ops.Geom(nx=NX, ny=NY, gx0=ox, gy0=oy)
+        a = ops.Field(lx, ly, k, gpu)
+        b = ops.Field(lx, ly, k, gpu)
+        ops.init_field(a, g, "random", seed)
+        ops.init_field(b, g, "random", seed)
+        levels = _cpu_levels(ops.Geom(nx=NX, ny=NY), NX, NY, 1, k, seed,
+                             box=(ox, ox + lx, oy, oy + ly))
+    for rl in range(1, k + 1):
+        resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+        ops.tb_step(a, b, g, k, resid=resid, variant=variant, res_level=rl)
+        torch.cuda.synchronize()
+        assert torch.equal(b.owned().cpu(), levels[k]), rl
+        want = float((levels[rl] - levels[rl - 1]).abs().max())
+        assert ops.resid_value(resid) == want, (rl, ops.resid_value(resid), want)
+
+
+def test_tb_inner_level_residual_needs_support(gpu):
+    # Forced variants without inner-level residuals refuse instead of taking
+    # the wrong level.
+    g, a, b = _fields(64, 300, 12, gpu)
+    resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+    with pytest.raises(Exception, match="residual at step 5"):
+        ops.tb_step(a, b, g, 12, resid=resid, variant=DEF, res_level=5)
+
+
 @pytest.mark.parametrize("variant", [DEF, DEEP, V.RING3, DEF | V.LINEAR, DEEP | V.LINEAR])
 def test_tb_residual_propagates_nan_and_inf(gpu, variant):
     # The residual max is NaN-propagating: one non-finite cell reaches the

@@ -71,3 +71,64 @@ def test_rccl_autotune(gpu, tmp_path):
                    tmp_path, transport="rccl")
     assert res["choices"][0] == res["choices"][1]
     assert all("ms_per_1000_iters" in r for r in res["table"])
+
+
+@pytest.mark.parametrize("schedule", ["pipeline", "overlap"])
+def test_rccl_schedule_convergence_graph(gpu, tmp_path, schedule):
+    # The overlap schedules under graph capture with the residual all-reduce
+    # and the device-judged gate (mpi/...c:235-262): under capture the
+    # interior launch runs on the forked comm stream and is joined before the
+    # all-reduce reads the residual word (Solver::enqueue_pass).
+    kw = dict(nx=64, ny=48, steps=40000, converge=True, check_interval=20, eps=1e-3,
+              init="ref-wrap", backend="hip", tb_depth=8, decomp="rows", schedule=schedule,
+              use_graph=True)
+    res = run_world(2, kw, 40000, tmp_path, transport="rccl")
+    ref, r, _ = single(kw, 40000)
+    assert str(res["schedule"]) == schedule
+    assert r.converged and bool(res["conv"])
+    assert int(res["conv_at"]) == r.converged_at and int(res["done"]) == r.steps_done
+    assert np.array_equal(res["grid"], ref)
+
+
+def test_rccl_dead_peer_fails_fast(gpu, tmp_path):
+    # Rank 1 dies at its 4th transport call (HEAT_TEST_FAIL_AFTER=3: the
+    # warm-up exchange and all-reduce pass, the first captured segment does
+    # not).  Rank 0 has launched that segment and waits on the device for
+    # halo rows that never come; its watchdog (HEAT_WATCHDOG_S) aborts the
+    # communicator and the process exits non-zero instead of hanging like
+    # the reference's MPI_Allreduce (mpi/...c:255) would.
+    import os
+    import subprocess
+    import time
+
+    from parallel_heat_amd import _native
+
+    from .dist_worker import free_port
+
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+                WORLD_SIZE="2", HEAT_WATCHDOG_S="10", NCCL_SOCKET_IFNAME="lo",
+                NCCL_IB_DISABLE="1")
+    cmd = [str(_native.CLI_PATH), "--backend", "hip", "--nx", "512", "--ny", "256",
+           "--steps", "2000000", "--converge", "--check-interval", "50", "--eps", "0",
+           "--decomp", "rows", "--out", "none", "--json"]
+    procs = []
+    for r in range(2):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), NCCL_HOSTID=f"heat-rank-{r}")
+        if r == 1:
+            env["HEAT_TEST_FAIL_AFTER"] = "3"
+        procs.append(subprocess.Popen(cmd, env=env, cwd=tmp_path, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    t0 = time.time()
+    try:
+        out1, err1 = procs[1].communicate(timeout=60)
+        out0, err0 = procs[0].communicate(timeout=60)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    elapsed = time.time() - t0
+    assert procs[1].returncode != 0 and "injected transport failure" in err1, err1[-2000:]
+    assert procs[0].returncode != 0, (out0[-500:], err0[-2000:])
+    assert "no progress" in err0 or "RCCL" in err0 or "aborted" in err0, err0[-2000:]
+    assert elapsed < 60
