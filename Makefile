@@ -32,8 +32,9 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp
 	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -x hip -c $< -o $@
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
-$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o \
-  $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o $(BUILD)/obj/tb_resident.o \
+  $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o \
+  $(BUILD)/obj/tb_split_mixed.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)

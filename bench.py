@@ -28,10 +28,18 @@ non-zero.
 Multi-GPU autotune (`--no-autotune` skips it): before the warmup, every
 decomposition candidate (rows slabs, the 2-D MPI_Dims_create grid) x pass
 schedule (deep-halo sync with the default and a halved exchange interval,
-boundary-first pipeline overlapping the exchange with the interior) is timed
-for two steps on the real ranks (max over ranks) and the fastest is
-benchmarked; the table is in the JSON line ("autotune") and the
-choice in config.parallelism.
+boundary-first pipeline overlapping the exchange with the interior) that the
+scaling model (parallel/model.py) does not rule out (predicted > 1.3x the
+best) is timed on the real ranks (max over ranks) and the fastest is
+benchmarked; the table is in the JSON line ("autotune", the ruled-out ones
+in "autotune_pruned") and the choice in config.parallelism.
+
+Multi-GPU explanation (after verification, untimed): "predicted" is the
+model's time per 1000 iterations and node Tcells/s for the chosen layout
+(per-rank plate rate measured on one GPU + a stated xGMI exchange model,
+parameters in "model"), and "phase_seconds_per_1000" the per-rank exchange /
+compute / reduce device time of one eager phase-timed run of the same
+configuration (Heat.pdf p.8-11 Paraver phases, as numbers).
 
 Failure handling: RCCL must come up on every rank (the ranks agree through
 torch.distributed before going on); if it fails anywhere the run exits
@@ -215,17 +223,22 @@ def main() -> int:
             shared = EngineTransport("torch", info, group=dist.new_group(backend="gloo"))
 
     tuning = None
+    pruned = []
     if world > 1 and not args.no_autotune:
         # The fastest decomposition (rows slabs vs the 2-D dims_create grid)
         # and pass schedule depend on xGMI link bandwidth and the per-rank
         # block shape: time each on the real ranks before the timed region.
-        from parallel_heat_amd.parallel.tune import autotune, default_candidates
+        from parallel_heat_amd.parallel.model import predict, prune
+        from parallel_heat_amd.parallel.tune import autotune, default_candidates, describe
 
         watchdog("autotune", args.watchdog_s)
-        cands = default_candidates(cfg, world,
-                                   schedules=[x for x in args.autotune_schedules.split(",") if x],
-                                   halo_passes=[int(x) for x in
-                                                args.autotune_halo_passes.split(",") if x])
+        all_cands = default_candidates(cfg, world,
+                                       schedules=[x for x in args.autotune_schedules.split(",") if x],
+                                       halo_passes=[int(x) for x in
+                                                    args.autotune_halo_passes.split(",") if x])
+        cands = prune(all_cands, world)
+        pruned = [dict(describe(c, world), predicted_ms_per_1000=predict(c, world)["ms_per_1000"])
+                  for c in all_cands if c not in cands]
         try:
             cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=3,
                                    log=(lambda m: log(rank, m)) if args.verbose else None,
@@ -276,6 +289,12 @@ def main() -> int:
     if not args.no_verify:
         watchdog("verify", args.watchdog_s)
         verified, check = verify(solver, cfg, rank, world, device, HeatSolver, DistInfo)
+    explain = None
+    if world > 1:
+        # Untimed: the model's prediction for the chosen layout and the
+        # measured per-rank phase split of one eager phase-timed run.
+        watchdog("explain", args.watchdog_s)
+        explain = explain_run(cfg, info, shared, world, args.iters_per_step, HeatSolver)
     rccl = None
     if shared is not None:
         # What the engine's communicator saw, from every rank: its rank count
@@ -328,6 +347,10 @@ def main() -> int:
         }
         if tuning is not None:
             line["autotune"] = tuning
+            if pruned:
+                line["autotune_pruned"] = pruned
+        if explain is not None:
+            line.update(explain)
         if rccl is not None:
             line["rccl"] = rccl
         if check:
@@ -345,6 +368,27 @@ def main() -> int:
     if world > 1:
         dist.destroy_process_group()
     return 0 if verified is not False else 2
+
+
+def explain_run(cfg, info, shared, world, iters, HeatSolver):
+    """Model prediction + measured per-rank phase split (collective)."""
+    from parallel_heat_amd.parallel.model import model_params, predict
+    phases = {"exchange": None, "compute": None, "reduce": None}
+    try:
+        with HeatSolver(cfg.replace(phase_timing=True), dist_info=info, shared=shared) as s:
+            r = s.run(iters)
+            scale = 1000.0 / max(1, r.steps_done)
+            phases = {"exchange": round(r.t_exchange * scale, 6),
+                      "compute": round(r.t_compute * scale, 6),
+                      "reduce": round(r.t_reduce * scale, 6),
+                      "wall": round(r.seconds * scale, 6),
+                      "resident_passes": r.resident_passes}
+    except Exception as e:  # noqa: BLE001 - diagnostics only; every rank still gathers
+        phases["error"] = str(e)[:200]
+    every = [None] * world
+    dist.all_gather_object(every, dict(phases, rank=info.rank))
+    return {"predicted": predict(cfg, world), "model": model_params(),
+            "phase_seconds_per_1000": every}
 
 
 def verify(solver, cfg, rank, world, device, HeatSolver, DistInfo):

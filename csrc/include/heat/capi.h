@@ -64,6 +64,7 @@ typedef struct heat_run_stats {
   double seconds;
   int64_t passes, exchanges, checks;
   double t_exchange, t_compute, t_reduce; /* seconds per phase (phase_timing) */
+  int64_t resident_passes;                /* passes run inside resident-tile launches */
 } heat_run_stats;
 
 typedef struct heat_block_info {

@@ -61,6 +61,7 @@ enum : int {
   kTile = 131072,       // workgroup tiles: 8 waves x R rows of a strip in VGPRs,
                         // neighbour rows through LDS each step (tbw, tb_tile.hip)
   kTileDpp = 262144,    // with kTile: DPP lane shifts instead of ds_bpermute
+  kShiftMixed = 524288, // with kSplit: west shift DPP, east ds_bpermute (tbxm, tb_split_mixed.hip)
   // Defaults: depth <= 8 and small launches at 12; large launches at 12.
   kDefault = kRamp | kScalar | kXcdGroups,  // 23
   kDefaultDeep = kDefault | kSplit,         // 2071
@@ -127,6 +128,25 @@ void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& bo
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1,
              int res_level = 0);
+// Resident workgroup tiles (tb_resident.hip): `passes` passes of `depth`
+// steps over ONE box in a single launch whose tiles stay in VGPRs, trading
+// only their K-deep ghost rings between passes through two exchange fields
+// (same layout as the field) and per-tile flags.  The tiles of the box must
+// all be co-resident (tb_resident_fits).  src is read by the first pass only;
+// dst (may equal src when passes is even) receives the last pass's box.
+struct TbResidentBuffers {
+  float* base[2] = {nullptr, nullptr};  // exchange field allocations
+  int64_t origin = 0;                   // owned cell (0, 0) in floats from base
+  int64_t bytes = 0;                    // allocation size
+  unsigned* flags = nullptr;            // >= max_tiles words, 16-byte aligned
+  int max_tiles = 0;
+  unsigned* err = nullptr;              // set non-zero if a neighbour wait gave up
+};
+bool tb_resident_fits(const Box& box, int depth, int variant = -1);
+void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
+                      int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,
+                      int variant = -1);
+
 // The automatic variant choice at this depth takes a residual at any inner
 // level (depth 12: level-split pipelines or workgroup tiles), so a
 // convergence check can ride inside a full-depth pass instead of cutting it.

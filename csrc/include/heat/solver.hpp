@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "heat/io.hpp"
+#include "heat/kernels.hpp"
 #include "heat/params.hpp"
 #include "heat/topology.hpp"
 #include "heat/transport.hpp"
@@ -55,6 +56,7 @@ struct RunStats {
   // Per-phase time (Params::phase_timing; device event time on the GPU,
   // summed over launches, so concurrent phases may add up to > seconds).
   double t_exchange = 0.0, t_compute = 0.0, t_reduce = 0.0;
+  int64_t resident_passes = 0;  // passes run inside resident-tile launches
 };
 
 class Solver {
@@ -149,6 +151,14 @@ class Solver {
   bool mid_residual_ok(int k) const;
   void enqueue_segment(const std::vector<PassPlan>& plan);
   void enqueue_pass(int k, int rl);
+  // Resident tiles: passes [i, i + n) of the plan in ONE launch whose tiles
+  // stay in VGPRs (gpu::tb_resident_step).  resident_span returns n (0: not
+  // eligible): same depth, no check, no exchange after the first pass, and
+  // every tile of the first pass's box co-resident.
+  int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
+  static int device_users(int dev);  // live GPU solvers of this process on dev
+  void enqueue_resident(int k, int n);
+  gpu::StencilGeom geom() const;
   void exchange(int buf, int k, hipStream_t st);
   // `st`: the stream to launch on (nullptr = the compute stream).
   void compute_gpu(int k, int rl, bool split, int part, int band = 0, int64_t er = 0,
@@ -191,6 +201,12 @@ class Solver {
   bool staged_ = false;  // GPU fields but host-memory transport
   bool host_checks_ = false;
   bool warmed_ = false;    // RCCL connections established outside capture
+  bool resident_ = false;  // resident-tile launches enabled for this solver
+  bool resident_force_ = false;  // HEAT_TB_RESIDENT=2: also with ranks sharing the device
+  bool resident_used_ = false;  // one was enqueued in this run (check its error word)
+  float* xbase_[2] = {nullptr, nullptr};  // their exchange fields
+  unsigned* d_flags_ = nullptr;           // + per-tile flags and the error word
+  unsigned* h_err_ = nullptr;             // pinned copy of the error word
   bool watch_ = false;     // multi-rank GPU run: waits poll with a watchdog
   double watchdog_s_ = 300.0;
   std::atomic<bool> aborted_{false};
@@ -199,7 +215,7 @@ class Solver {
   int cur_ = 0;
   int64_t step_ = 0;
   float cpu_resid_ = 0.f;
-  int64_t stat_passes_ = 0, stat_exchanges_ = 0;
+  int64_t stat_passes_ = 0, stat_exchanges_ = 0, stat_resident_ = 0;
 
   float* base_[2] = {nullptr, nullptr};
   float* field_[2] = {nullptr, nullptr};
@@ -209,6 +225,7 @@ class Solver {
   float* cn_[8] = {};
   // Host staging (staged_ mode), one pair per message of an exchange.
   static constexpr int kMaxMsgs = 8;
+  static constexpr size_t kResidentFlagBytes = 16384;  // flags of up to 4096 resident tiles
   float* stage_send_[kMaxMsgs] = {};
   float* stage_recv_[kMaxMsgs] = {};
   size_t stage_bytes_ = 0;
@@ -225,6 +242,8 @@ class Solver {
     int cur_after = 0;
     int64_t gr_after = 0, gc_after = 0;
     int64_t passes = 0, exchanges = 0;
+    bool resident = false;         // holds a resident-tile launch (check its error word)
+    int64_t resident_passes = 0;
     std::vector<PassRec> recs;     // relative to the segment's first step
     std::vector<int64_t> checks;   // check steps (relative), in judge order
   };

@@ -368,7 +368,9 @@ int tb_resident_waves(int depth, int variant) {
   const int lag = tb_variant_lag(variant);
   if (tb_variant_split(variant)) {
     // Work units are two-wave pipelines, two per block.
-    const int w = std::max(1, cus * std::max(1, tbx::occupancy_split(depth)) * 2);
+    const int occ = (variant & tbv::kShiftMixed) ? tbxm::occupancy_split(depth)
+                                                 : tbx::occupancy_split(depth);
+    const int w = std::max(1, cus * std::max(1, occ) * 2);
     cache.emplace(key, w);
     return w;
   }
@@ -727,7 +729,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
                (long long)sb.waves, (long long)need);
     args.stamps = sb.buf;
   }
-  const bool ok = split                      ? tbx::launch_split(args, depth, st)
+  const bool ok = split ? ((variant & tbv::kShiftMixed) ? tbxm::launch_split(args, depth, st)
+                                                        : tbx::launch_split(args, depth, st))
                   : (variant & tbv::kFloat2) ? tbn::launch(args, depth, lag, st)
                   : (variant & tbv::kScalar) ? tbs::launch(args, depth, lag, st)
                                              : tbp::launch(args, depth, lag, st);

@@ -134,6 +134,10 @@ bool launch_split_rl_a(const tbdetail::TbArgs& args, int depth, int rl, hipStrea
 bool launch_split_rl_b(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 bool launch_split_rl_c(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 }
+namespace heat::gpu::tbxm {  // level-split pipelines, mixed DPP / ds_bpermute shifts (tb_split_mixed.hip)
+bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);
+int occupancy_split(int depth);
+}
 namespace heat::gpu::tbn {  // float2 lanes (tb_narrow.hip)
 bool launch(const tbdetail::TbArgs& args, int depth, int lag, hipStream_t st);
 int occupancy(int depth, int lag);

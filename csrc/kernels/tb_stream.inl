@@ -49,6 +49,14 @@ using heat::gpu::tbdetail::kSplitRing;
 // don't-care.  bound_ctrl lets the compiler fold both shifts into the
 // consuming v_add_f32_dpp; with old = 0 and bound_ctrl off it only folded
 // wave_shr and materialised wave_shl as v_mov 0 + v_mov_b32_dpp + v_add.
+// A DPP wave shift left (lane l <- lane l-1), folded by the compiler into
+// the consuming v_add_f32_dpp: the left shift of the mixed build
+// (HEAT_TB_BPERMUTE 2), which sends only the right shift through the LDS
+// crossbar (the workgroup-tile kernel measured +3-6 % for that split of the
+// two shifts between the VALU and LDS pipes, profiles/r3_tile.md).
+__device__ __forceinline__ float dpp_wave_shr(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
 #if HEAT_TB_BPERMUTE
 // Lane shifts through the LDS crossbar (ds_bpermute_b32, no LDS memory):
 // DPP wave shifts mixed into the FMA stream stop a second wave per SIMD from
@@ -375,7 +383,15 @@ struct TbStream {
     } else {
       L0[modn<6>(T6 + 3)] = load_row(src, FAST ? i + 3 : min(i + 3, last_in), pitch);
     }
-#if HEAT_TB_BPERMUTE
+#if HEAT_TB_BPERMUTE == 2
+    // Mixed: the K right shifts through the LDS crossbar, issued up front;
+    // each left shift a DPP wave shift at its use (folded into the add).
+    float er[K + 1];
+#pragma unroll
+    for (int s = 1; s <= K; ++s) er[s] = dpp_from_right(lv(s - 1, T6 - s)[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#define HEAT_TB_UPD(s, a_, b_, c_, ok_) upd.apply(a_, b_, c_, dpp_wave_shr((b_)[V - 1]), er[s], ok_)
+#elif HEAT_TB_BPERMUTE
     // Every level's centre row (level s-1, row t - s) was produced in an
     // earlier iteration: issue all 2K lane shifts (LDS crossbar round trips)
     // up front so their latencies overlap, instead of each level waiting on
@@ -712,7 +728,12 @@ __device__ __forceinline__ int64_t tb_lin_boundary(const TbArgs& a, int64_t x) {
 // group of G chunks split between G units).  Linear plans: a range of the
 // strip-row sequence, run as consecutive segments (a strip end, a box end
 // or a row where the Dirichlet mode changes starts a new segment).
-template <int K, int LAG, int K1, int RLM = 0>
+// LIN: 0 classic plans only, 1 linear plans only, 2 either (the launch's
+// kTbLinear flag at run time).  The level-split launches instantiate 0 and 1
+// separately, so the classic kernel carries no inlined copy of the linear
+// segment loop (its register allocation and ramp spills stay those of the
+// classic body alone).
+template <int K, int LAG, int K1, int RLM = 0, int LIN = 2>
 __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int stage, vecf* ring,
                                        unsigned* cnt, unsigned* wg, int nact) {
   constexpr int K2 = K - K1;
@@ -721,7 +742,7 @@ __device__ __forceinline__ void tb_run(const TbArgs& a, int wave, int age, int s
   const unsigned long long t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   float m = 0.f;
   int strip = 0, chunk = wave;
-  const bool linear = a.flags & tbdetail::kTbLinear;
+  const bool linear = LIN == 2 ? bool(a.flags & tbdetail::kTbLinear) : LIN == 1;
   int64_t x0 = 0, x1 = 1;  // linear: this unit's strip-row range
   if (linear) {
     const int64_t U = a.total_waves;
@@ -828,7 +849,7 @@ template <int K, int K1>
 constexpr int tb_split_waves_per_simd() {
   return tb_waves_per_simd<(K1 > K - K1 ? K1 : K - K1), 3>();
 }
-template <int K, int K1, int RLM = 0>
+template <int K, int K1, int RLM = 0, int LIN = 2>
 __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_split_kernel(TbArgs a) {
   __shared__ vecf ring[2][kSplitRing * 64];
   __shared__ unsigned cnt[2][2];
@@ -848,7 +869,7 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_sp
     nact += tb_unit(a, 2, q, ag) < a.total_waves ? 1 : 0;
   }
   if (unit >= a.total_waves) return;
-  tb_run<K, 3, K1, RLM>(a, unit, age, wid & 1, ring[p], cnt[p], wg, nact);
+  tb_run<K, 3, K1, RLM, LIN>(a, unit, age, wid & 1, ring[p], cnt[p], wg, nact);
 }
 #endif
 
@@ -879,7 +900,7 @@ int occ_k() {
   return std::max(1, n);
 }
 
-#if !HEAT_TB_SPLIT_RL_LO  // the residual-level units define only their launcher
+#if !HEAT_TB_SPLIT_RL_LO && !HEAT_TB_SPLIT_ONLY  // those units define only split launchers
 // Resident 256-thread blocks per CU of the (depth, lag) instantiation.
 int occupancy(int depth, int lag) {
 #if HEAT_TB_DEEP
@@ -958,11 +979,11 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
 #endif  // !HEAT_TB_SPLIT_RL_LO
 
 #if HEAT_TB_SPLIT
-template <int K, int K1, int RLM = 0>
+template <int K, int K1, int RLM = 0, int LIN = 2>
 void launch_split_k(const TbArgs& args, hipStream_t st) {
   int blocks = int((args.total_waves + 1) / 2);  // two pipelines per block
   if (args.flags & tbdetail::kTbAgePairs) blocks = (blocks + 7) / 8 * 8 * args.age_groups;
-  hipLaunchKernelGGL((tb_split_kernel<K, K1, RLM>), dim3(blocks), dim3(256), 0, st, args);
+  hipLaunchKernelGGL((tb_split_kernel<K, K1, RLM, LIN>), dim3(blocks), dim3(256), 0, st, args);
 }
 #endif
 #if HEAT_TB_SPLIT_RL_LO
@@ -989,10 +1010,10 @@ bool HEAT_TB_SPLIT_RL_FN(const TbArgs& args, int depth, int rl, hipStream_t st) 
 template <int K, int K1>
 int occ_split_k() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tb_split_kernel<K, K1>, 256, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tb_split_kernel<K, K1, 0, 0>, 256, 0) != hipSuccess)
     n = 1;
   hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tb_split_kernel<K, K1>)) == hipSuccess &&
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tb_split_kernel<K, K1, 0, 0>)) == hipSuccess &&
       fa.numRegs > 0) {
     const int alloc = (fa.numRegs + 7) / 8 * 8;
     n = std::min(n, std::min(8, 512 / alloc));
@@ -1006,11 +1027,17 @@ int occ_split_k() {
 bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
   const int rl = args.res_level;
   if (args.resid != nullptr && rl > 0 && rl < depth)  // a check inside the pass
-    return launch_split_rl_a(args, depth, rl, st) || launch_split_rl_b(args, depth, rl, st) ||
-           launch_split_rl_c(args, depth, rl, st);
+    return tbx::launch_split_rl_a(args, depth, rl, st) || tbx::launch_split_rl_b(args, depth, rl, st) ||
+           tbx::launch_split_rl_c(args, depth, rl, st);
   switch (depth) {
-    case 8: launch_split_k<8, 4>(args, st); return true;
-    case 12: launch_split_k<12, 6>(args, st); return true;
+    case 8:
+      if (args.flags & tbdetail::kTbLinear) launch_split_k<8, 4, 0, 1>(args, st);
+      else launch_split_k<8, 4, 0, 0>(args, st);
+      return true;
+    case 12:
+      if (args.flags & tbdetail::kTbLinear) launch_split_k<12, 6, 0, 1>(args, st);
+      else launch_split_k<12, 6, 0, 0>(args, st);
+      return true;
     default: return false;
   }
 }

@@ -281,6 +281,7 @@ int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out) {
       out->passes = r.passes;
       out->exchanges = r.exchanges;
       out->checks = r.checks;
+      out->resident_passes = r.resident_passes;
     }
   });
 }

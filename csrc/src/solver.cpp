@@ -38,6 +38,18 @@ void host_unpack(const float* buf, float* origin, int64_t pitch, const Box& b) {
 
 }  // namespace
 
+namespace {
+// Solvers of this process per GPU (resident launches need the device alone).
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_users;
+}  // namespace
+
+int Solver::device_users(int dev) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto it = g_dev_users.find(dev);
+  return it == g_dev_users.end() ? 0 : it->second;
+}
+
 Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
     : P_(p), tr_(maybe_inject_faults(std::move(tr))) {
   HEAT_CHECK(tr_ != nullptr, "no transport");
@@ -100,6 +112,23 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
     sched_ = Schedule::Sync;
   L_ = Layout::make(blk_.lx, blk_.ly, H_);
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
+  // Resident tiles for the workgroup-tile shapes (small per-rank blocks):
+  // even depths, the synchronous schedule, the automatic variant choice;
+  // HEAT_TB_RESIDENT=0 restores one launch per pass.
+  // The resident grid must own its device: never with ranks sharing one GPU
+  // (loopback threads, or several processes per GPU as in the RCCL
+  // rehearsal), where two resident grids could each hold CUs the other's
+  // tiles wait for.  Multi-rank runs therefore need a device per rank in
+  // sight (device count >= world) and no other solver of this process on
+  // the device (resident_span).  HEAT_TB_RESIDENT=2 skips that check (tests
+  // whose ranks' grids all fit the one GPU together), 0 disables.
+  int ndev = 0;
+  if (on_gpu() && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  const int res_env = env_int("HEAT_TB_RESIDENT", 1);
+  resident_force_ = res_env == 2;
+  resident_ = tile_sized() && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
+              !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
+              (world == 1 || ndev >= world || resident_force_);
   host_checks_ = env_int("HEAT_HOST_CHECKS", 0) != 0;
   timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
   // Waits on the device poll the transport and give up after this long
@@ -113,9 +142,19 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
     free_all();  // the destructor does not run for a throwing constructor
     throw;
   }
+  if (on_gpu()) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    ++g_dev_users[P_.device >= 0 ? P_.device : 0];
+  }
 }
 
-Solver::~Solver() { free_all(); }
+Solver::~Solver() {
+  if (on_gpu()) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    --g_dev_users[P_.device >= 0 ? P_.device : 0];
+  }
+  free_all();
+}
 
 void Solver::alloc() {
   const size_t ew_elems = size_t(blk_.lx) * size_t(H_);
@@ -145,6 +184,13 @@ void Solver::alloc() {
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
+    if (resident_) {
+      for (auto& b : xbase_) HIP_CHECK(hipMalloc(&b, size_t(L_.bytes())));
+      HIP_CHECK(hipMalloc(&d_flags_, kResidentFlagBytes + 256));
+      HIP_CHECK(hipMemset(d_flags_, 0, kResidentFlagBytes + 256));
+      HIP_CHECK(hipHostMalloc(&h_err_, 256));
+      *h_err_ = 0;
+    }
     HIP_CHECK(hipMalloc(&d_gate_, sizeof(gpu::DeviceGate)));
     HIP_CHECK(hipMemset(d_gate_, 0, sizeof(gpu::DeviceGate)));
     HIP_CHECK(hipHostMalloc(&h_gate_, 2 * sizeof(gpu::DeviceGate)));
@@ -205,6 +251,10 @@ void Solver::free_all() {
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_checksum_) (void)hipFree(d_checksum_);
     if (d_gate_) (void)hipFree(d_gate_);
+    for (auto& b : xbase_)
+      if (b) (void)hipFree(b);
+    if (d_flags_) (void)hipFree(d_flags_);
+    if (h_err_) (void)hipHostFree(h_err_);
     if (h_gate_) (void)hipHostFree(h_gate_);
     for (auto e : {ev_ready_, ev_halo_, ev_wait_, ev_seg_[0], ev_seg_[1]})
       if (e) (void)hipEventDestroy(e);
@@ -225,6 +275,9 @@ void Solver::free_all() {
   h_resid_ = nullptr;
   d_scratch_ = d_checksum_ = nullptr;
   d_gate_ = h_gate_ = nullptr;
+  xbase_[0] = xbase_[1] = nullptr;
+  d_flags_ = nullptr;
+  h_err_ = nullptr;
   ev_ready_ = ev_halo_ = ev_wait_ = ev_seg_[0] = ev_seg_[1] = nullptr;
   s_comp_ = s_comm_ = nullptr;
 }
@@ -507,16 +560,7 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
   PhaseScope phase(this, kCompute, st);
   const float* src = field_[cur_];
   float* dst = field_[cur_ ^ 1];
-  gpu::StencilGeom g;
-  g.pitch = L_.pitch;
-  g.gx0 = blk_.ox;
-  g.gy0 = blk_.oy;
-  g.nx = P_.nx;
-  g.ny = P_.ny;
-  g.cx = P_.cx;
-  g.cy = P_.cy;
-  g.numerics = int(P_.numerics);
-  if (gated()) g.gate = static_cast<const unsigned*>(d_gate_);  // DeviceGate::stop
+  const gpu::StencilGeom g = geom();
   unsigned* r = rl > 0 ? d_resid_ : nullptr;
   const int64_t lx = blk_.lx, ly = blk_.ly;
   const auto& nb = blk_.nbr;
@@ -565,6 +609,93 @@ void Solver::compute_gpu(int k, int rl, bool split, int part, int band, int64_t 
     gpu::tb_step(src, dst, g, b, 4, k, r, st, waves_target, -1, rl);
     // cur_ flips once per pass, after the boundary part.
   }
+}
+
+gpu::StencilGeom Solver::geom() const {
+  gpu::StencilGeom g;
+  g.pitch = L_.pitch;
+  g.gx0 = blk_.ox;
+  g.gy0 = blk_.oy;
+  g.nx = P_.nx;
+  g.ny = P_.ny;
+  g.cx = P_.cx;
+  g.cy = P_.cy;
+  g.numerics = int(P_.numerics);
+  if (gated()) g.gate = static_cast<const unsigned*>(d_gate_);  // DeviceGate::stop
+  return g;
+}
+
+int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
+  if (!resident_ || plan[i].k != T_ || plan[i].rl != 0) return 0;
+  if (tr_->world() > 1 && !resident_force_ && device_users(P_.device >= 0 ? P_.device : 0) > 1)
+    return 0;
+  const int k = T_;
+  const bool ns = cart_.px > 1, ew = cart_.py > 1;
+  // Ghost validity after the first pass's (possible) exchange, then the
+  // bookkeeping of ensure_ghosts pass by pass: the span ends before a pass
+  // that would need an exchange, or a check.
+  int64_t gr = gr_, gc = gc_;
+  if ((ns && gr < k) || (ew && gc < k)) gr = gc = H_;
+  const Box box{blk_.nbr[North] >= 0 ? -(ns ? gr - k : 0) : 0,
+                blk_.lx + (blk_.nbr[South] >= 0 ? (ns ? gr - k : 0) : 0),
+                blk_.nbr[West] >= 0 ? -(ew ? round_down(gc - k, 4) : 0) : 0,
+                blk_.ly + (blk_.nbr[East] >= 0 ? (ew ? round_down(gc - k, 4) : 0) : 0)};
+  int n = 0;
+  for (size_t j = i; j < plan.size(); ++j) {
+    if (plan[j].k != k || plan[j].rl != 0) break;
+    if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
+    if (ns) gr -= k;
+    if (ew) gc = round_down(gc - k, 4);
+    ++n;
+  }
+  if (n < 2 || !gpu::tb_resident_fits(box, k)) return 0;
+  return n;
+}
+
+void Solver::enqueue_resident(int k, int n) {
+  TraceRange trace("heat.resident");
+  // The first pass's exchange (if its ghosts ran out) and box; the later
+  // passes only shrink the ghost validity (resident_span checked that none
+  // of them needs an exchange).  The launch computes the first box in every
+  // pass: cells it cannot keep valid lie outside each later pass's box, in
+  // ghost columns and rows the bookkeeping already treats as stale.
+  const int64_t ex0 = stat_exchanges_;
+  const auto ext = ensure_ghosts(k, s_comp_);
+  const auto& nb = blk_.nbr;
+  const Box box{nb[North] >= 0 ? -ext.first : 0, blk_.lx + (nb[South] >= 0 ? ext.first : 0),
+                nb[West] >= 0 ? -ext.second : 0, blk_.ly + (nb[East] >= 0 ? ext.second : 0)};
+  for (int j = 1; j < n; ++j) (void)ensure_ghosts(k, s_comp_);
+  HEAT_CHECK(stat_exchanges_ - ex0 <= 1, "resident span of %d passes needs an exchange", n);
+  const int cur0 = cur_;
+  const int out = cur_ ^ (n & 1);
+  {
+    PhaseScope phase(this, kCompute, s_comp_);
+    gpu::TbResidentBuffers xb;
+    xb.base[0] = xbase_[0];
+    xb.base[1] = xbase_[1];
+    xb.origin = L_.origin();
+    xb.bytes = L_.bytes();
+    xb.flags = d_flags_;
+    xb.max_tiles = int(kResidentFlagBytes / 4);
+    xb.err = d_flags_ + kResidentFlagBytes / 4;
+    gpu::tb_resident_step(field_[cur_], field_[out], geom(), box, k, n, xb, s_comp_);
+  }
+  resident_used_ = true;
+  for (int j = 0; j < n; ++j) {
+    PassRec rec;
+    rec.step0 = step_ + int64_t(j) * k;
+    rec.k = k;
+    rec.rl = 0;
+    rec.cur0 = j == 0 ? cur0 : out;
+    rec.cur1 = out;
+    rec.gr1 = gr_;
+    rec.gc1 = gc_;
+    pass_log_.push_back(rec);
+  }
+  cur_ = out;
+  step_ += int64_t(n) * k;
+  stat_passes_ += n;
+  stat_resident_ += n;
 }
 
 void Solver::compute_cpu(int k, int rl, int64_t er, int64_t ec) {
@@ -746,7 +877,16 @@ void Solver::enqueue_pass(int k, int rl) {
 }
 
 void Solver::enqueue_segment(const std::vector<PassPlan>& plan) {
-  for (const PassPlan& p : plan) enqueue_pass(p.k, p.rl);
+  for (size_t i = 0; i < plan.size();) {
+    const int n = on_gpu() ? resident_span(plan, i) : 0;
+    if (n >= 2) {
+      enqueue_resident(plan[i].k, n);
+      i += size_t(n);
+    } else {
+      enqueue_pass(plan[i].k, plan[i].rl);
+      ++i;
+    }
+  }
   if (comm_pending_) {
     // Join the comm stream (the last pass posted the next exchange): a
     // captured graph must end on its origin stream, and the next segment
@@ -870,7 +1010,9 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
   const auto key = std::make_tuple(n, phase, cur_, gr_, gc_);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
-    const int64_t p_before = stat_passes_, e_before = stat_exchanges_;
+    const int64_t p_before = stat_passes_, e_before = stat_exchanges_, r_before = stat_resident_;
+    const bool res_before = resident_used_;
+    resident_used_ = false;
     TraceRange trace_capture("heat.capture");
     hipGraph_t graph;
     HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
@@ -893,18 +1035,24 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
     e.gc_after = gc_;
     e.passes = stat_passes_ - p_before;
     e.exchanges = stat_exchanges_ - e_before;
+    e.resident = resident_used_;
+    e.resident_passes = stat_resident_ - r_before;
+    stat_resident_ = r_before;
+    resident_used_ = res_before;
     relative(e);
     stat_passes_ = p_before;
     stat_exchanges_ = e_before;
     it = graphs_.emplace(key, std::move(e)).first;
   }
   HIP_CHECK(hipGraphLaunch(it->second.exec, s_comp_));
+  resident_used_ = resident_used_ || it->second.resident;
   cur_ = it->second.cur_after;
   gr_ = it->second.gr_after;
   gc_ = it->second.gc_after;
   step_ = step_before + n;
   stat_passes_ += it->second.passes;
   stat_exchanges_ += it->second.exchanges;
+  stat_resident_ += it->second.resident_passes;
   *recs = it->second.recs;
   *checks = it->second.checks;
 }
@@ -1051,7 +1199,7 @@ RunStats Solver::run(int64_t steps) {
   TraceRange trace("heat.run");
   RunStats s;
   HEAT_CHECK(steps >= 0, "negative step count");
-  const int64_t p0 = stat_passes_, e0 = stat_exchanges_;
+  const int64_t p0 = stat_passes_, e0 = stat_exchanges_, res0 = stat_resident_;
   synchronize();
   const double t0 = now_s();
   const bool gpu = on_gpu();
@@ -1069,11 +1217,19 @@ RunStats Solver::run(int64_t steps) {
     sync_watch();
     warmed_ = true;
   }
+  resident_used_ = false;
   if (steps > 0) {
     if (gated()) run_gated(steps, s);
     else run_segments(steps, s);
   }
+  if (resident_used_)
+    HIP_CHECK(hipMemcpyAsync(h_err_, d_flags_ + kResidentFlagBytes / 4, 4, hipMemcpyDeviceToHost,
+                             s_comp_));
   sync_watch();
+  if (resident_used_ && *h_err_ != 0)
+    throw_error(__FILE__, __LINE__,
+                "resident tile launch: a neighbour wait gave up (tiles not co-resident?); "
+                "results are invalid (HEAT_TB_RESIDENT=0 runs one launch per pass)");
   check_staged();
   tr_->check();
   s.seconds = now_s() - t0;
@@ -1086,6 +1242,7 @@ RunStats Solver::run(int64_t steps) {
   s.total_steps = step_;
   s.passes = stat_passes_ - p0;
   s.exchanges = stat_exchanges_ - e0;
+  s.resident_passes = stat_resident_ - res0;
   return s;
 }
 

@@ -82,6 +82,7 @@ class HeatRunStats(Structure):
         ("last_resid", c_float), ("seconds", c_double),
         ("passes", c_int64), ("exchanges", c_int64), ("checks", c_int64),
         ("t_exchange", c_double), ("t_compute", c_double), ("t_reduce", c_double),
+        ("resident_passes", c_int64),
     ]
 
 

@@ -39,6 +39,7 @@ class RunResult:
     t_exchange: float = 0.0  # seconds in halo exchanges (phase_timing)
     t_compute: float = 0.0   # seconds in stencil kernels
     t_reduce: float = 0.0    # seconds in residual all-reduce + read-back
+    resident_passes: int = 0  # passes run inside resident-tile launches (tiles kept in VGPRs)
 
     @property
     def mcells_per_s(self) -> float:
@@ -185,7 +186,7 @@ class HeatSolver:
         return RunResult(st.steps_done, st.total_steps, bool(st.converged), st.converged_at,
                          st.last_resid, st.seconds, st.passes, st.exchanges, st.checks,
                          self.config.nx * self.config.ny, st.t_exchange, st.t_compute,
-                         st.t_reduce)
+                         st.t_reduce, st.resident_passes)
 
     def reset(self) -> None:
         _native.call("heat_solver_reset", self._h)

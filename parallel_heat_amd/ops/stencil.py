@@ -46,6 +46,7 @@ class TbVariant(enum.IntFlag):
     NO_LINEAR = 65536     # never switch to it (default: when the classic plan fills < 90 %)
     TILE = 131072         # workgroup tiles: 8 waves x R rows in VGPRs, LDS row exchange per step
     TILE_DPP = 262144     # with TILE: DPP lane shifts instead of ds_bpermute
+    SHIFT_MIXED = 524288  # with SPLIT: west shift DPP, east ds_bpermute (tb_split_mixed.hip)
     DEFAULT = RAMP | SCALAR | XCD_GROUPS       # 23
     DEFAULT_DEEP = DEFAULT | SPLIT             # 2071
 

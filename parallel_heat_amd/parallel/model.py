@@ -1,0 +1,150 @@
+"""Strong-scaling model of a decomposed run on one MI355X node.
+
+The reference quantifies its MPI scaling by hand (Heat.pdf p.5 Table 1:
+speedup and efficiency at 1 and 10 machines; p.8-11 Paraver phases).  Here
+the same accounting is a model that ``bench.py`` prints next to the measured
+multi-GPU number, and that the autotune uses to skip candidates it rules out:
+
+    time per 1000 iterations = compute(per-rank block) + exchanges x t_exchange
+                               + checks x t_allreduce
+
+* compute: the per-rank block's cells (plus the deep-halo ghost rows it
+  recomputes) at the rate one MI355X reaches on a plate of that shape.  The
+  rates are this build's measured whole-solver ``bench.py`` plates whose top
+  and bottom rows are plate edges (the slowest rank of a decomposition,
+  which the max over ranks reports), interpolated in strip-rows per SIMD --
+  the planner's own measure of the work per launch (RATE_POINTS).
+* exchange: one grouped RCCL send/recv phase per m*K steps (deep halos),
+  every message on its own xGMI link (full mesh, one hop): a fixed latency
+  plus the largest message over the link bandwidth (XGMI).  2-D grids add
+  the pack / unpack launches of the E/W columns and ghost corners.
+* all-reduce: one 4-byte ncclAllReduce(max) per convergence check.
+
+All parameters are stated in ``XGMI`` / ``RATE_POINTS`` and returned with
+every prediction, so a measured SCALE record can be read against them.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence
+
+from ..models.config import HeatConfig
+from .topology import dims_create
+
+# Exchange cost model on the xGMI full mesh (7 links x ~153 GB/s per GPU,
+# SURVEY §2.4).  Latency: a grouped ncclSend/ncclRecv phase captured in a
+# graph is O(10 us) of launch + protocol; bandwidth: the effective one-way
+# rate RCCL's P2P transport reaches on one link at 0.1-1 MB messages.
+XGMI = {
+    "latency_us": 12.0,          # per grouped exchange phase
+    "link_gbps": 50.0,           # effective GB/s per link and direction
+    "pack_us": 3.0,              # per pack or unpack launch (2-D grids: 2 per exchange)
+    "allreduce_us": 12.0,        # one 4-byte ncclAllReduce(max) per check
+}
+
+# Whole-solver rate (Tcells/s of owned cells) of one MI355X on a bench plate
+# (plate edges top and bottom) vs strip-rows per SIMD of that plate (232
+# useful columns per 256-column strip at depth 12, 1024 SIMDs).  Measured
+# with this build: profiles/r4_resident.md (1024 x 8192 and 2048 x 4096:
+# resident workgroup tiles), profiles/r3_tile.md (2048 x 8192, 4096 x 4096,
+# 4096 x 8192), BENCH (8192 x 8192).
+RATE_POINTS: List[tuple] = [
+    # (strip-rows per SIMD, Tcells/s)
+    (18.0, 2.6),    # 512 x 8192 (16-GPU-like blocks; extrapolated from the tile trend)
+    (36.0, 3.9),    # 1024 x 8192 / 2048 x 4096 (8 GPUs), resident tiles
+    (72.0, 3.75),   # 2048 x 8192 / 4096 x 4096 (4 GPUs), split pipelines
+    (144.0, 4.6),   # 4096 x 8192 (2 GPUs)
+    (288.0, 5.0),   # 8192 x 8192 (1 GPU)
+]
+
+SIMDS = 1024
+STRIP_COLS = 232  # useful columns per 256-column strip at depth 12
+
+
+def rate_tcells(rows: int, cols: int) -> float:
+    """Interpolated whole-solver rate of a rows x cols block (Tcells/s)."""
+    srps = math.ceil(cols / STRIP_COLS) * rows / SIMDS
+    pts = RATE_POINTS
+    if srps <= pts[0][0]:
+        return pts[0][1] * srps / pts[0][0] if srps > 0 else pts[0][1]
+    for (x0, y0), (x1, y1) in zip(pts, pts[1:]):
+        if srps <= x1:
+            return y0 + (y1 - y0) * (srps - x0) / (x1 - x0)
+    return pts[-1][1]
+
+
+def _grid(cfg: HeatConfig, world: int) -> tuple:
+    if cfg.px > 0 and cfg.py > 0:
+        return cfg.px, cfg.py
+    if cfg.decomp in ("rows", "1d"):
+        return world, 1
+    d = dims_create(world, 2)
+    return d[0], d[1]
+
+
+def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8) -> Dict:
+    """Predicted time per 1000 iterations and node throughput of cfg on
+    `world` GPUs (the slowest rank: the largest block, with neighbours)."""
+    px, py = _grid(cfg, world)
+    lx = math.ceil(cfg.nx / px)
+    ly = math.ceil(cfg.ny / py)
+    m = cfg.halo_passes or halo_passes
+    if world == 1:
+        m = 1
+    schedule = cfg.schedule if cfg.schedule != "auto" else "sync"
+    if world > 1 and schedule != "sync":
+        m = 1
+    H = m * depth
+    # Deep-halo ghost rows recomputed on the decomposed axes (both sides of an
+    # inner rank): the first pass's box (resident launches keep it for all m
+    # passes).
+    ext_r = 2 * (H - depth) if px > 1 else 0
+    ext_c = 2 * (H - depth) if py > 1 else 0
+    rate = rate_tcells(lx, ly) * 1e12
+    cells = (lx + ext_r) * (ly + ext_c)
+    compute_s = cells * 1000 / rate
+    exchanges = math.ceil(1000 / H) if world > 1 else 0
+    ns_bytes = H * (ly + 2 * H) * 4 if px > 1 else 0
+    ew_bytes = lx * H * 4 if py > 1 else 0
+    msg = max(ns_bytes, ew_bytes)
+    t_ex = (XGMI["latency_us"] * 1e-6 + msg / (XGMI["link_gbps"] * 1e9) +
+            (2 * XGMI["pack_us"] * 1e-6 if py > 1 else 0.0))
+    ex_total = exchanges * t_ex
+    if schedule != "sync" and world > 1:
+        # Overlap schedules: one K-deep exchange per pass, hidden behind the
+        # interior launch, but the boundary bands are separate latency-bound
+        # launches and every pass pays a cross-stream join (~10-15 us each,
+        # profiles/overlap_probe_r1.md); no resident spans (split kernels).
+        passes = math.ceil(1000 / depth)
+        per_pass = lx * ly * depth / (rate_tcells(lx, ly) * 1e12 * 0.8)
+        compute_s = passes * (max(per_pass, t_ex) + 25e-6)
+        ex_total = 0.0
+    checks = math.floor(1000 / cfg.check_interval) if cfg.converge else 0
+    reduce_s = checks * XGMI["allreduce_us"] * 1e-6 if world > 1 else 0.0
+    total = compute_s + ex_total + reduce_s
+    return {
+        "layout": f"{px}x{py}", "block": f"{lx}x{ly}", "schedule": schedule,
+        "halo": H, "exchanges_per_1000": exchanges,
+        "compute_ms": round(compute_s * 1e3, 4),
+        "exchange_ms": round(ex_total * 1e3, 4),
+        "reduce_ms": round(reduce_s * 1e3, 4),
+        "ms_per_1000": round(total * 1e3, 4),
+        "tcells_per_s": round(cfg.nx * cfg.ny * 1000 / total / 1e12, 3),
+        "rank_rate_tcells": round(rate_tcells(lx, ly), 3),
+        "message_bytes": msg,
+    }
+
+
+def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3) -> List[HeatConfig]:
+    """The candidates whose predicted time is within `slack` x the best
+    prediction (the autotune times only these)."""
+    if len(cands) <= 1:
+        return list(cands)
+    t = [predict(c, world)["ms_per_1000"] for c in cands]
+    best = min(t)
+    return [c for c, x in zip(cands, t) if x <= slack * best]
+
+
+def model_params() -> Dict:
+    return {"xgmi": dict(XGMI), "rate_points": [list(p) for p in RATE_POINTS],
+            "strip_cols": STRIP_COLS, "simds": SIMDS}

@@ -365,3 +365,22 @@ def test_mfma_step_tiling_invariance(gpu):
         ops.mfma_step(a, b2, g, box)
     torch.cuda.synchronize()
     assert torch.equal(b1.owned(), b2.owned())
+
+
+MIXED = DEEP | V.SHIFT_MIXED  # level-split pipelines, west shift DPP / east ds_bpermute
+
+
+@pytest.mark.parametrize("variant,depth", [(MIXED, 12), (MIXED, 8), (MIXED | V.ALT_DIRECTION, 12),
+                                           (MIXED | V.FORCE_AGE_PAIRS, 12), (MIXED | V.LINEAR, 12)])
+def test_tb_split_mixed_shifts_bitwise(gpu, depth, variant):
+    # tb_split_mixed.hip: the same pipelines with the west neighbour as a DPP
+    # wave shift: bitwise vs the CPU oracle, residual included.
+    for lx, ly in ((203, 517), (1000, 2000)):
+        g, a, b = _fields(lx, ly, depth, gpu)
+        resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+        ops.tb_step(a, b, g, depth, resid=resid, variant=variant)
+        torch.cuda.synchronize()
+        prev = _cpu_steps(g, lx, ly, depth, depth - 1)
+        ref = _cpu_steps(g, lx, ly, depth, depth)
+        assert torch.equal(b.owned().cpu(), ref), (lx, ly)
+        assert ops.resid_value(resid) == float((ref - prev).abs().max())

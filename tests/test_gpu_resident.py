@@ -1,0 +1,97 @@
+"""Resident workgroup tiles (csrc/kernels/tb_resident.hip): the passes between
+two halo exchanges (all passes of a segment on one rank) run as ONE launch
+whose tiles stay in VGPRs and trade only their K-deep ghost rings through
+flag-guarded exchange fields.  Bitwise against separate per-pass launches
+(HEAT_TB_RESIDENT=0) and the CPU oracle, on plates whose tiles touch every
+Dirichlet edge, odd shapes, deep-halo multi-rank blocks (loopback ranks,
+2-D grids with ghost corners), graph and eager, and checked runs (checks end
+a resident span).  Reference: the per-rank compute of
+mpi/mpi_heat_improved_persistent_stat.c:162-234.  Needs an MI355X."""
+import numpy as np
+import pytest
+
+from parallel_heat_amd import HeatConfig, HeatSolver
+from parallel_heat_amd.parallel.group import run_group
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(cfg, steps, resident, monkeypatch, chunks=None):
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "1" if resident else "0")
+    with HeatSolver(cfg) as s:
+        res = [s.run(n) for n in (chunks or [steps])]
+        return s.gather(), res
+
+
+@pytest.mark.parametrize("nx,ny,steps,fits", [
+    (1024, 8192, 100, True),    # the 8-GPU 1-D per-rank block as a plate
+    (2048, 4096, 60, True),     # the 8-GPU 2-D (4 x 2) per-rank block
+    (203, 517, 97, True),       # partial strips and tiles, a short remainder
+    (300, 1000, 50, True),
+    (40, 70, 36, True),         # fewer rows than one tile
+])
+def test_resident_plate_bitwise(gpu, monkeypatch, nx, ny, steps, fits):
+    cfg = HeatConfig(nx=nx, ny=ny, steps=steps, init="random", seed=11, backend="hip")
+    g1, r1 = _solve(cfg, steps, True, monkeypatch)
+    g0, r0 = _solve(cfg, steps, False, monkeypatch)
+    assert r0[0].resident_passes == 0
+    if fits:
+        assert r1[0].resident_passes >= 2, r1
+    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+    if nx * ny <= 1 << 20:
+        c, _ = _solve(cfg.replace(backend="cpu", tb_depth=1), steps, False, monkeypatch)
+        assert np.array_equal(g1, c), np.abs(g1 - c).max()
+
+
+def test_resident_repeated_runs_graph_and_eager(gpu, monkeypatch):
+    # bench.py's pattern: the same segment graph replayed (flags re-zeroed by
+    # the memset node every launch), and the eager path.
+    cfg = HeatConfig(nx=1024, ny=8192, steps=0, init="random", seed=3, backend="hip")
+    g_graph, rs = _solve(cfg, 0, True, monkeypatch, chunks=[240, 240, 240])
+    assert all(r.resident_passes > 0 for r in rs)
+    g_eager, _ = _solve(cfg.replace(use_graph=False), 0, True, monkeypatch,
+                        chunks=[240, 240, 240])
+    g_sep, _ = _solve(cfg, 0, False, monkeypatch, chunks=[240, 240, 240])
+    assert np.array_equal(g_graph, g_sep)
+    assert np.array_equal(g_eager, g_sep)
+
+
+@pytest.mark.parametrize("world,kw", [
+    (2, dict(nx=2048, ny=2048, decomp="rows")),         # 1024-row blocks, 96-row halos
+    (4, dict(nx=1024, ny=1024, px=2, py=2)),             # 2-D: E/W columns and ghost corners
+    (3, dict(nx=777, ny=900, decomp="rows")),            # uneven blocks, remainders
+])
+def test_resident_multirank_deep_halo(gpu, monkeypatch, world, kw):
+    # Ranks as threads of one process (loopback transport on the one GPU):
+    # each exchange refills an m*K-deep ring and the m passes behind it run
+    # as one resident launch over the first pass's (largest) box.  Ranks
+    # sharing a GPU never go resident by default (two resident grids could
+    # each hold CUs the other's tiles wait for); HEAT_TB_RESIDENT=2 forces it
+    # on blocks small enough that every rank's grid fits the GPU at once.
+    cfg = HeatConfig(steps=0, init="random", seed=5, backend="hip", **kw)
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "1")
+    res = run_group(cfg, world, lambda s: s.run(48))
+    assert all(r.resident_passes == 0 for r in res)  # shared device: not resident
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "2")
+    res = run_group(cfg, world, lambda s: (s.run(300), s.gather()))
+    assert all(r[0].resident_passes > 0 for r in res), [r[0] for r in res]
+    got = next(g for _, g in res if g is not None)
+    single = cfg.replace(decomp="auto", px=0, py=0)
+    want, _ = _solve(single, 300, False, monkeypatch)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+
+
+@pytest.mark.parametrize("interval", [50, 20, 7])
+def test_resident_with_checks(gpu, monkeypatch, interval):
+    # Checks are never inside a resident span (a check pass runs on its own,
+    # its residual possibly at an inner level); the spans between them stay
+    # resident.  Converges, bitwise vs the CPU oracle and vs separate passes.
+    cfg = HeatConfig(nx=96, ny=300, steps=40000, converge=True, check_interval=interval,
+                     eps=1e-3, init="ref-wrap", backend="hip", tb_depth=12)
+    g1, r1 = _solve(cfg, None, True, monkeypatch)
+    g0, r0 = _solve(cfg, None, False, monkeypatch)
+    c, rc = _solve(cfg.replace(backend="cpu", tb_depth=1), None, False, monkeypatch)
+    assert r1[0].converged and r1[0].converged_at == rc[0].converged_at == r0[0].converged_at
+    if interval >= 2 * 12:
+        assert r1[0].resident_passes > 0
+    assert np.array_equal(g1, c) and np.array_equal(g0, c)

@@ -26,3 +26,34 @@ def test_bench_candidates_2_ranks_one_layout():
 def test_halo_passes_only_for_sync():
     keys = _keys(4, schedules=["overlap"], halo_passes=[0, 4, 16])
     assert keys == [(4, 1, "overlap", 0), (2, 2, "overlap", 0)]
+
+
+def test_model_prunes_overlap_schedules_at_8_ranks():
+    # The scaling model (parallel/model.py) rules out the boundary-first
+    # pipeline on the 8-GPU blocks (per-pass band launches and joins, no
+    # resident spans) and keeps every deep-halo sync candidate.
+    from parallel_heat_amd.parallel.model import predict, prune
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    cands = default_candidates(cfg, 8, schedules=["sync", "pipeline"], halo_passes=[0, 4])
+    kept = [tuple(describe(c, 8).values()) for c in prune(cands, 8)]
+    assert kept == [(8, 1, "sync", 0), (8, 1, "sync", 4), (4, 2, "sync", 0), (4, 2, "sync", 4)]
+    p = predict(cands[0], 8)
+    assert p["layout"] == "8x1" and p["block"] == "1024x8192" and p["halo"] == 96
+    assert p["exchanges_per_1000"] == 11 and p["message_bytes"] == 96 * (8192 + 2 * 96) * 4
+    assert abs(p["ms_per_1000"] - (p["compute_ms"] + p["exchange_ms"])) < 1e-3
+    assert 0 < p["tcells_per_s"] < 8 * 5.5
+
+
+def test_model_single_gpu_is_the_plate_rate():
+    from parallel_heat_amd.parallel.model import RATE_POINTS, predict
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    p = predict(cfg, 1)
+    assert p["exchanges_per_1000"] == 0 and p["exchange_ms"] == 0
+    assert p["tcells_per_s"] == RATE_POINTS[-1][1]
+
+
+def test_model_more_ranks_never_slower_per_rank_block():
+    from parallel_heat_amd.parallel.model import rate_tcells
+    # Rates are monotone-ish in work per SIMD within the measured range.
+    assert rate_tcells(8192, 8192) >= rate_tcells(4096, 8192) >= rate_tcells(2048, 8192)
+    assert rate_tcells(512, 8192) < rate_tcells(1024, 8192)
