@@ -86,7 +86,7 @@ def test_resident_with_checks(gpu, monkeypatch, interval):
     # Checks are never inside a resident span (a check pass runs on its own,
     # its residual possibly at an inner level); the spans between them stay
     # resident.  Converges, bitwise vs the CPU oracle and vs separate passes.
-    cfg = HeatConfig(nx=96, ny=300, steps=40000, converge=True, check_interval=interval,
+    cfg = HeatConfig(nx=48, ny=96, steps=40000, converge=True, check_interval=interval,
                      eps=1e-3, init="ref-wrap", backend="hip", tb_depth=12)
     g1, r1 = _solve(cfg, None, True, monkeypatch)
     g0, r0 = _solve(cfg, None, False, monkeypatch)
