@@ -79,8 +79,11 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
     candidate rides the same communicator instead of one ncclCommInitRank per
     candidate.  Collective over torch.distributed's default group when
     info.world > 1: every rank takes the same sequence of agreements, so a
-    candidate that fails on any rank (construction or run) is skipped on all
-    of them together instead of leaving the ranks in mismatched collectives."""
+    candidate that any rank rejects at construction is skipped on all
+    of them together instead of leaving the ranks in mismatched collectives.
+    That holds for failures at construction only: a candidate that fails
+    while it runs aborts the (shared) transport and the whole autotune on
+    that rank (NativeError); its peers end in their watchdog."""
     import torch
     import torch.distributed as dist
 
@@ -134,29 +137,30 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             continue
         dt = 0.0
         try:
+            solver.run(steps)  # graph capture, RCCL connections
+            barrier()
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(repeats):
+                solver.run(steps)
+            sync()
+            dt = time.perf_counter() - t0
+            row["halo"] = solver.info.halo
+            row["tb_depth"] = solver.info.tb_depth
+        except _native.NativeError as e:
+            # A run-time failure can leave this rank's peers inside a send /
+            # recv / all-reduce that will never match, and unmatched ops queued
+            # on the shared communicator: no later candidate may use it.
+            # Abort it (ncclCommAbort: the peers' pending waits end in their
+            # watchdog, HEAT_WATCHDOG_S) and end the whole autotune.
             try:
-                solver.run(steps)  # graph capture, RCCL connections
-                barrier()
-                sync()
-                t0 = time.perf_counter()
-                for _ in range(repeats):
-                    solver.run(steps)
-                sync()
-                dt = time.perf_counter() - t0
-                row["halo"] = solver.info.halo
-                row["tb_depth"] = solver.info.tb_depth
-                ok = 1.0
-            except _native.NativeError as e:
-                ok = 0.0
-                row["error"] = str(e).splitlines()[0][:200]
-        finally:
-            solver.close()
-        if agree_all(ok, MIN) < 1.0:
-            row.setdefault("error", "failed on another rank")
-            table.append(row)
-            if log:
-                log(f"autotune: {row} failed")
-            continue
+                solver.abort()
+            finally:
+                solver.close()
+            raise _native.NativeError(
+                f"autotune aborted: candidate {row} failed at run time on rank "
+                f"{info.rank}: {str(e).splitlines()[0][:200]}") from e
+        solver.close()
         dt = agree_all(dt, MAX)
         ms = dt * 1e3 * 1000.0 / (steps * repeats)
         row["ms_per_1000_iters"] = round(ms, 4)

@@ -1,7 +1,9 @@
 """Candidate set of the multi-GPU autotune (parallel/tune.py) as bench.py
 builds it: rows slabs and the MPI_Dims_create grid, x deep-halo sync with the
 default and a doubled exchange interval, x the boundary-first pipeline."""
-from parallel_heat_amd import HeatConfig
+import pytest
+
+from parallel_heat_amd import HeatConfig, _native
 from parallel_heat_amd.parallel.tune import default_candidates, describe
 
 
@@ -57,3 +59,49 @@ def test_model_more_ranks_never_slower_per_rank_block():
     # Rates are monotone-ish in work per SIMD within the measured range.
     assert rate_tcells(8192, 8192) >= rate_tcells(4096, 8192) >= rate_tcells(2048, 8192)
     assert rate_tcells(512, 8192) < rate_tcells(1024, 8192)
+
+
+class _FakeSolver:
+    """Stands in for HeatSolver: construction outcome and run outcome chosen
+    per candidate schedule."""
+    aborted = []
+
+    def __init__(self, cfg, fail_make=False, fail_run=False):
+        if fail_make:
+            raise _native.NativeError("block thinner than its halo")
+        self.cfg, self.fail_run = cfg, fail_run
+        self.info = type("I", (), {"halo": 12, "tb_depth": 12})()
+
+    def run(self, n):
+        if self.fail_run:
+            raise _native.NativeError("planner check failed mid-run")
+
+    def abort(self):
+        _FakeSolver.aborted.append(self.cfg.schedule)
+
+    def close(self):
+        pass
+
+
+def _tune(fails):
+    from parallel_heat_amd.parallel.comm import DistInfo
+    from parallel_heat_amd.parallel.tune import autotune
+    cfg = HeatConfig(nx=64, ny=64, backend="cpu")
+    cands = [cfg.replace(schedule=s) for s in ("sync", "pipeline", "overlap")]
+    make = lambda c: _FakeSolver(c, **fails.get(c.schedule, {}))  # noqa: E731
+    return autotune(cfg, DistInfo(0, 1, 0), candidates=cands, steps=2, repeats=1, make=make)
+
+
+def test_autotune_skips_a_candidate_rejected_at_construction():
+    best, table = _tune({"sync": dict(fail_make=True)})
+    assert "error" in table[0] and "ms_per_1000_iters" in table[1]
+    assert best.schedule in ("pipeline", "overlap")
+
+
+def test_autotune_aborts_on_a_run_time_failure():
+    # The shared communicator may hold unmatched ops after a mid-run failure:
+    # the transport is aborted and no later candidate runs.
+    _FakeSolver.aborted.clear()
+    with pytest.raises(_native.NativeError, match="autotune aborted"):
+        _tune({"pipeline": dict(fail_run=True)})
+    assert _FakeSolver.aborted == ["pipeline"]
