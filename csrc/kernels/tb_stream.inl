@@ -667,6 +667,7 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.qoff = qoff;
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb - K2, re + K2, rlo, rhi, store_lane, upd);
+      m = st.m;  // an inner-level residual of stage 0's levels (RS_ST0)
     } else {
       TbStream<K2, LAG, MD, RS_ST1, 2> st;
       st.lo = V * lane;
