@@ -61,6 +61,8 @@ struct ResArgs {
   int xbytes;           // allocation size (buffer descriptor range, < 2^31)
   unsigned* flags;      // one word per tile, zeroed before the launch
   unsigned* err;        // non-zero: a neighbour wait gave up (bounded spin)
+  int diag;             // timing diagnostics (HEAT_TB_RES_DIAG, wrong results):
+                        // bit 0 no neighbour wait, 1 no ghost reload, 2 no publish
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -174,7 +176,9 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     int xr0 = xrow0, xp = xpitch;
     opaque32(xr0);
     opaque32(xp);
-    Pub pub{xr[p & 1], usemask, bandmask, store_lane, band_lane, vlane, xr0, xp};
+    const bool nopub = ra.diag & 4;
+    Pub pub{xr[p & 1], usemask, nopub ? 0u : bandmask, nopub ? false : store_lane,
+            nopub ? false : band_lane, vlane, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
     auto xstep = [&](auto down_c, auto what_c, int s) {
@@ -198,7 +202,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
 
   // Wait for the neighbours' pass p - 1 bands, then reload the ghost ring.
   auto refill = [&](int p) {
-    if (w == 0) {
+    if (w == 0 && !(ra.diag & 1)) {
       // Wave 0, one lane per neighbour tile: relaxed agent-scope polls
       // (sc1), bounded; a give-up is reported, never waited out.
       const int ns = bx.nstrips, nc = bx.nchunks;
@@ -219,6 +223,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       }
     }
     __syncthreads();
+    if (ra.diag & 2) return;
     const __amdgpu_buffer_rsrc_t rs = xr[(p - 1) & 1];
     unsigned gm = ghostmask, um = usemask;
     opaque(gm);
@@ -437,6 +442,7 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   ra.xbytes = int(xb.bytes);
   ra.flags = xb.flags;
   ra.err = xb.err;
+  ra.diag = tune.res_diag;
   // Re-initialise every call: the flags (a memset node under capture).
   HIP_CHECK(hipMemsetAsync(xb.flags, 0, size_t(round_up(int64_t(pl.units) * 4, 16)), st));
   if (const char* e = std::getenv("HEAT_TB_TRACE"); e && *e && *e != '0') {

@@ -123,7 +123,7 @@ def test_cli_single_process_rccl(gpu, tmp_path):
     if ndev < 2:
         p = subprocess.run([str(_native.CLI_PATH), "--gpus", "2", "--transport", "rccl"] + args,
                            cwd=tmp_path, capture_output=True, text=True, timeout=120)
-        assert p.returncode == 2 and "needs 2 GPUs" in p.stderr
+        assert p.returncode == 2 and "one GPU per rank" in p.stderr, p.stderr
         return
     hashes = {}
     for n in (1, 2):
