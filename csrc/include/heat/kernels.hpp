@@ -133,7 +133,9 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // only their K-deep ghost rings between passes through two exchange fields
 // (same layout as the field) and per-tile flags.  The tiles of the box must
 // all be co-resident (tb_resident_fits).  src is read by the first pass only;
-// dst (may equal src when passes is even) receives the last pass's box.
+// dst receives the last pass's box.  resid: the max |delta| of the LAST
+// pass's step res_level (1..depth; a check that ends the span) over the owned
+// block [0, own_rows) x [0, own_cols) only (nullptr: none).
 struct TbResidentBuffers {
   float* base[2] = {nullptr, nullptr};  // exchange field allocations
   int64_t origin = 0;                   // owned cell (0, 0) in floats from base
@@ -145,7 +147,8 @@ struct TbResidentBuffers {
 bool tb_resident_fits(const Box& box, int depth, int variant = -1);
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                       int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,
-                      int variant = -1);
+                      int variant = -1, unsigned* resid = nullptr, int res_level = 0,
+                      int64_t own_rows = 0, int64_t own_cols = 0);
 
 // The automatic variant choice at this depth takes a residual at any inner
 // level (depth 12: level-split pipelines or workgroup tiles), so a

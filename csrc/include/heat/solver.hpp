@@ -136,6 +136,10 @@ class Solver {
     int k = 0, rl = 0;
     int cur0 = 0, cur1 = 0;
     int64_t gr1 = 0, gc1 = 0;
+    // A check that ends a resident span: the span's passes (cur0 = its
+    // source buffer) and box growth (er, ec), for replay_check.
+    int span = 1;
+    int64_t er = 0, ec = 0;
   };
   void alloc();
   void free_all();
@@ -157,7 +161,7 @@ class Solver {
   // every tile of the first pass's box co-resident.
   int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
   static int device_users(int dev);  // live GPU solvers of this process on dev
-  void enqueue_resident(int k, int n);
+  void enqueue_resident(int k, int n, int rl_last);
   gpu::StencilGeom geom() const;
   void exchange(int buf, int k, hipStream_t st);
   // `st`: the stream to launch on (nullptr = the compute stream).

@@ -61,6 +61,7 @@ struct ResArgs {
   int xbytes;           // allocation size (buffer descriptor range, < 2^31)
   unsigned* flags;      // one word per tile, zeroed before the launch
   unsigned* err;        // non-zero: a neighbour wait gave up (bounded spin)
+  int64_t own_r1, own_c1;  // owned block [0, own_r1) x [0, own_c1): the residual's cells
   int diag;             // timing diagnostics (HEAT_TB_RES_DIAG, wrong results):
                         // bit 0 no neighbour wait, 1 no ghost reload, 2 no publish
 };
@@ -70,8 +71,12 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // Neighbour waits give up after this many polls (~0.3 s with s_sleep 2).
 constexpr unsigned kSpinLimit = 1u << 22;
 
-template <int R, int NW, int MODE, int XL>
-__device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
+// RES 1: the residual of the LAST pass (a check that ends the span) at its
+// step a.res_level, under a uniform row mask that is zero in every other
+// step (tb_tile_core.hpp).  Returns this lane's max.  A separate
+// instantiation: the RES 0 kernel keeps its register allocation.
+template <int R, int NW, int MODE, int XL, int RES>
+__device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
                                              int u, vecf (*xch)[2][NW][64]) {
   const TbArgs& a = ra.a;
   const int K = ra.depth;
@@ -94,7 +99,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
   float* __restrict__ dst = a.dst + (cbase - KK);
   const int lo = 4 * lane;
 
-  Tile<R, MODE, 0, XL> T;
+  Tile<R, MODE, RES, XL> T;
   auto ld = [&](int r) {
     int64_t row = min(max(row0 + r, rmin), rmax);
     opaque(row);
@@ -132,6 +137,10 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
   const bool band_lane = store_lane && (col < cbase + KK || col + 4 > cend - KK);
   const bool ghost_lane = !store_lane && col >= bx.c0 && col < bx.c1;
   const bool box_lane = col >= bx.c0 && col < bx.c1;
+  // The last pass's residual: owned cells only (a deep-halo box's edge rows
+  // and columns are stale by then).
+  const unsigned resmask = bits(max<int64_t>(ub, 0) - row0, min<int64_t>(ue, ra.own_r1) - row0);
+  const int res_rc = store_lane && col >= 0 && col < ra.own_c1 ? int(min<int64_t>(ra.own_c1 - col, 4)) : 0;
   // Exchange fields through buffer descriptors (sc1 = write-through stores,
   // L2-coherent loads): the lane's column in the voffset VGPR, the row in the
   // scalar soffset.  Row offsets derive from a base made opaque once per
@@ -181,6 +190,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
             nopub ? false : band_lane, vlane, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
+    const int rs = LAST && RES ? a.res_level - 1 : -1;
     auto xstep = [&](auto down_c, auto what_c, int s) {
       constexpr bool D = decltype(down_c)::value;
       xc.p = s & 1;
@@ -188,15 +198,18 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       const vecf first_nb = xc.efirst;
       opaque(rowmask);
       opaque(usemask);
+      unsigned rm = s == rs ? resmask : 0u;
+      opaque(rm);
       T.template step<D, decltype(what_c)::value>(first_nb, xc, up, rowmask, usemask, store_lane,
-                                                   rc, dst + lo, off0, pitch, &pub);
+                                                   rc, dst + lo, off0, pitch, &pub, rm, res_rc);
     };
+    using Plain = std::integral_constant<int, 0>;
     int s = 0;
     for (; s + 2 < K; s += 2) {
-      xstep(Down{}, std::integral_constant<int, 0>{}, s);
-      xstep(Up{}, std::integral_constant<int, 0>{}, s + 1);
+      xstep(Down{}, Plain{}, s);
+      xstep(Up{}, Plain{}, s + 1);
     }
-    xstep(Down{}, std::integral_constant<int, 0>{}, s);
+    xstep(Down{}, Plain{}, s);
     xstep(Up{}, std::integral_constant<int, LAST ? 1 : 3>{}, s + 1);
   };
 
@@ -253,9 +266,10 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
   }
   refill(P - 1);
   pass(std::true_type{}, P - 1);
+  return T.m;
 }
 
-template <int R, int NW, int XL>
+template <int R, int NW, int XL, int RES>
 __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_resident_kernel(
     ResArgs ra) {
   __shared__ vecf xch[2][2][NW][64];  // [step parity][first / last row][wave][lane]
@@ -276,18 +290,34 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
   const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
   const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
-  if (interior) resident_run<R, NW, 0, XL>(ra, bx, strip, t, blk, xch);
-  else resident_run<R, NW, 1, XL>(ra, bx, strip, t, blk, xch);
+  const float m = interior ? resident_run<R, NW, 0, XL, RES>(ra, bx, strip, t, blk, xch)
+                           : resident_run<R, NW, 1, XL, RES>(ra, bx, strip, t, blk, xch);
+  if constexpr (RES == 1) {
+    // One atomic per workgroup (tb_tile.hip): non-negative floats (and NaN,
+    // sign cleared by fabs) order like their bit patterns.
+    __shared__ unsigned wmax[NW];
+    unsigned mm = __float_as_uint(m);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mm = max(mm, unsigned(__shfl_xor(int(mm), off)));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned r = 0u;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) r = max(r, wmax[i]);
+      atomicMax(a.resid, r);
+    }
+  }
 }
 
 template <int R, int NW, int XL>
 int occ_res() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_resident_kernel<R, NW, XL>, 64 * NW, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_resident_kernel<R, NW, XL, 0>, 64 * NW, 0) !=
       hipSuccess)
     n = 1;
   hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_resident_kernel<R, NW, XL>)) ==
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_resident_kernel<R, NW, XL, 0>)) ==
           hipSuccess &&
       fa.numRegs > 0) {
     const int alloc = (fa.numRegs + 7) / 8 * 8;
@@ -311,16 +341,21 @@ int occupancy_res(int rows, int waves, int xl) {
   return 0;
 }
 
+template <int R, int NW, int XL>
+void launch_res_x(const ResArgs& ra, int blocks, hipStream_t st) {
+  if (ra.a.resid != nullptr)
+    hipLaunchKernelGGL((tile_resident_kernel<R, NW, XL, 1>), dim3(blocks), dim3(64 * NW), 0, st, ra);
+  else
+    hipLaunchKernelGGL((tile_resident_kernel<R, NW, XL, 0>), dim3(blocks), dim3(64 * NW), 0, st, ra);
+}
+
 bool launch_res(const ResArgs& ra, int rows, int waves, int xl, int blocks, hipStream_t st) {
-#define HEAT_RES_CASE(r, nw)                                                                     \
-  if (rows == r && waves == nw) {                                                                \
-    if (xl == 1)                                                                                 \
-      hipLaunchKernelGGL((tile_resident_kernel<r, nw, 1>), dim3(blocks), dim3(64 * nw), 0, st, ra); \
-    else if (xl == 2)                                                                            \
-      hipLaunchKernelGGL((tile_resident_kernel<r, nw, 2>), dim3(blocks), dim3(64 * nw), 0, st, ra); \
-    else                                                                                         \
-      hipLaunchKernelGGL((tile_resident_kernel<r, nw, 0>), dim3(blocks), dim3(64 * nw), 0, st, ra); \
-    return true;                                                                                 \
+#define HEAT_RES_CASE(r, nw)                                          \
+  if (rows == r && waves == nw) {                                     \
+    if (xl == 1) launch_res_x<r, nw, 1>(ra, blocks, st);              \
+    else if (xl == 2) launch_res_x<r, nw, 2>(ra, blocks, st);         \
+    else launch_res_x<r, nw, 0>(ra, blocks, st);                      \
+    return true;                                                      \
   }
   HEAT_RES_SHAPES(HEAT_RES_CASE)
 #undef HEAT_RES_CASE
@@ -400,7 +435,8 @@ bool tb_resident_fits(const Box& box, int depth, int variant) {
 
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                       int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,
-                      int variant) {
+                      int variant, unsigned* resid, int res_level, int64_t own_rows,
+                      int64_t own_cols) {
   using namespace tbw;
   HEAT_CHECK(passes >= 2, "a resident launch spans >= 2 passes (%d)", passes);
   const TbTuning tune = tb_tuning();
@@ -417,8 +453,10 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   TbArgs& a = ra.a;
   a.src = src;
   a.dst = dst;
-  a.resid = nullptr;
-  a.res_level = depth;
+  HEAT_CHECK(resid == nullptr || (res_level >= 1 && res_level <= depth),
+             "resident residual at step %d of a depth-%d pass", res_level, depth);
+  a.resid = resid;
+  a.res_level = resid ? res_level : depth;
   a.g = g;
   a.flags = (variant < 0 || (variant & tbv::kXcdGroups)) ? tbdetail::kTbXcdGroups : 0;
   TbBox& t = a.box[0];
@@ -442,6 +480,8 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   ra.xbytes = int(xb.bytes);
   ra.flags = xb.flags;
   ra.err = xb.err;
+  ra.own_r1 = resid ? own_rows : box.r1;
+  ra.own_c1 = resid ? own_cols : box.c1;
   ra.diag = tune.res_diag;
   // Re-initialise every call: the flags (a memset node under capture).
   HIP_CHECK(hipMemsetAsync(xb.flags, 0, size_t(round_up(int64_t(pl.units) * 4, 16)), st));

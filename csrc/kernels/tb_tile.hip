@@ -108,6 +108,8 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   xch[1][1][w][lane] = T.u[0];
   lds_barrier();
   xc.efirst = xch[1][0][wa][lane];
+  // RES 1: the residual of step res_level - 1 (uniform mask, zero elsewhere).
+  const int rs = RES ? a.res_level - 1 : -1;
   auto xstep = [&](auto down_c, auto last_c, int s) {
     constexpr bool D = decltype(down_c)::value;
     xc.p = s & 1;
@@ -116,41 +118,32 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
     const vecf first_nb = xc.efirst;
     opaque(rowmask);
     opaque(usemask);
+    unsigned rm = s == rs ? ~0u : 0u;
+    opaque(rm);
     T.template step<D, decltype(last_c)::value>(first_nb, xc, up, rowmask, usemask, store_lane, rc,
-                                                 dst + lo, off0, pitch);
+                                                 dst + lo, off0, pitch,
+                                                 static_cast<TileNoSink*>(nullptr), rm);
   };
   using Down = std::true_type;
   using Up = std::false_type;
   using Plain = std::integral_constant<int, 0>;
   using Last = std::integral_constant<int, 1>;
-  using Mid = std::integral_constant<int, 2>;
-  // Steps in (down, up) pairs (K is even, see launch()); the residual rides
-  // on the last up step (RES 1) or on step res_level - 1 (RES 2: a uniform
-  // branch per step picks the body that accumulates it).
+  // Steps in (down, up) pairs (K is even, see launch()).
   int s = 0;
-  if constexpr (RES == 2) {
-    const int rs = a.res_level - 1;
-    for (; s + 2 < K; s += 2) {
-      if (s == rs) xstep(Down{}, Mid{}, s);
-      else xstep(Down{}, Plain{}, s);
-      if (s + 1 == rs) xstep(Up{}, Mid{}, s + 1);
-      else xstep(Up{}, Plain{}, s + 1);
-    }
-    if (s == rs) xstep(Down{}, Mid{}, s);
-    else xstep(Down{}, Plain{}, s);
-  } else {
-    for (; s + 2 < K; s += 2) {
-      xstep(Down{}, Plain{}, s);
-      xstep(Up{}, Plain{}, s + 1);
-    }
+  for (; s + 2 < K; s += 2) {
     xstep(Down{}, Plain{}, s);
+    xstep(Up{}, Plain{}, s + 1);
   }
+  xstep(Down{}, Plain{}, s);
   xstep(Up{}, Last{}, s + 1);
   return T.m;
 }
 
 
-template <int R, int NW, int XL>
+// RES: 0 no residual; 1 the residual of step a.res_level (check passes).
+// Separate instantiations: the residual must not cost the plain passes
+// registers (one kernel with both bodies spilled 240-680 B per lane).
+template <int R, int NW, int XL, int RES>
 __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_kernel(TbArgs a, int K) {
   __shared__ vecf xch[2][2][NW][64];  // [step parity][first / last row][wave][lane]
   if (tbdetail::gated(a.g.gate)) return;  // uniform over the launch
@@ -177,19 +170,9 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
   const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
   const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
-  float m;
-  // Residual: none, on the last step, or on an inner step (res_level).
-  const int res = a.resid == nullptr ? 0 : (a.res_level > 0 && a.res_level < K) ? 2 : 1;
-  if (interior) {
-    m = res == 0 ? tile_run<R, NW, 0, 0, XL>(a, bx, strip, t, K, xch)
-        : res == 1 ? tile_run<R, NW, 0, 1, XL>(a, bx, strip, t, K, xch)
-                   : tile_run<R, NW, 0, 2, XL>(a, bx, strip, t, K, xch);
-  } else {
-    m = res == 0 ? tile_run<R, NW, 1, 0, XL>(a, bx, strip, t, K, xch)
-        : res == 1 ? tile_run<R, NW, 1, 1, XL>(a, bx, strip, t, K, xch)
-                   : tile_run<R, NW, 1, 2, XL>(a, bx, strip, t, K, xch);
-  }
-  if (a.resid != nullptr) {
+  const float m = interior ? tile_run<R, NW, 0, RES, XL>(a, bx, strip, t, K, xch)
+                           : tile_run<R, NW, 1, RES, XL>(a, bx, strip, t, K, xch);
+  if constexpr (RES == 1) {
     // One atomic per workgroup: a per-wave atomicMax on the one residual
     // word from ~4000 waves serialised at the memory side (~37 us per check
     // pass at 1024 x 8192, as much as the whole pass).  Non-negative floats
@@ -211,18 +194,22 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
 
 template <int R, int NW, int XL>
 void launch_r(const TbArgs& args, int depth, hipStream_t st) {
-  hipLaunchKernelGGL((tile_kernel<R, NW, XL>), dim3(args.total_waves), dim3(64 * NW), 0, st, args,
-                     depth);
+  if (args.resid != nullptr)
+    hipLaunchKernelGGL((tile_kernel<R, NW, XL, 1>), dim3(args.total_waves), dim3(64 * NW), 0, st,
+                       args, depth);
+  else
+    hipLaunchKernelGGL((tile_kernel<R, NW, XL, 0>), dim3(args.total_waves), dim3(64 * NW), 0, st,
+                       args, depth);
 }
 
 template <int R, int NW, int XL>
 int occ_r() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_kernel<R, NW, XL>, 64 * NW, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_kernel<R, NW, XL, 0>, 64 * NW, 0) != hipSuccess)
     n = 1;
   // Bound by the VGPR granule as well (the API can over-report by one block).
   hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_kernel<R, NW, XL>)) == hipSuccess &&
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_kernel<R, NW, XL, 0>)) == hipSuccess &&
       fa.numRegs > 0) {
     const int alloc = (fa.numRegs + 7) / 8 * 8;
     n = std::min(n, (512 / alloc) / (NW / 4));

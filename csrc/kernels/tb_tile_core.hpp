@@ -101,8 +101,9 @@ struct Upd {
 
 struct TileNoSink;
 
-// RES: 0 no residual, 1 residual on the last step (with the stores), 2 on
-// an inner step (TbArgs::res_level, a check inside a full-depth pass).
+// RES: 0 no residual; 1 max |new - old| over the rows of `resmask` (a
+// runtime mask: zero except in the step that takes the check's residual,
+// TbArgs::res_level, the last step or an inner one of a full-depth pass).
 template <int R, int MODE, int RES, int XL>
 struct Tile {
   vecf u[R];
@@ -119,15 +120,20 @@ struct Tile {
   // direction only needed a copy of every row per step at the back-edge.
   // WHAT 1 (LAST): the launch's last step stores every useful row as soon as
   // it is computed (dst + off0 + r * pitch, this lane's columns if
-  // store_lane) and, with RES 1, accumulates max |new - old| over the useful
-  // cells; WHAT 2: an inner step that only accumulates the residual (RES 2);
-  // WHAT 3: every row goes to sink->row(r, new, old) (the resident kernel's
-  // edge-band publish, tb_resident.hip).
+  // store_lane); WHAT 3: every row goes to sink->row(r, new, old) (the
+  // resident kernel's edge-band publish, tb_resident.hip).  With RES 1 any
+  // step accumulates max |new - old| over the useful rows in resmask.
   template <bool DOWN, int WHAT, class Xc, class Sink = TileNoSink>
   __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, XL>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
                                        float* __restrict__ dst, int64_t off0, int64_t pitch,
-                                       Sink* sink = nullptr) {
+                                       Sink* sink = nullptr, unsigned resmask = ~0u,
+                                       int res_rc = -1) {
+    // Residual window (the resident kernel's deep-halo boxes: the owned block
+    // only): rows resmask, res_rc useful columns of this lane (-1: the stored
+    // cells, store_lane / rc).
+    const bool res_lane = res_rc < 0 ? store_lane : res_rc > 0;
+    const int res_cols = res_rc < 0 ? rc : res_rc;
     // Lane shifts of the OLD rows.  ds_bpermute results take ~50+ cycles: the
     // shifts of the row PD places ahead in processing order are issued before
     // a row is computed (scheduling barriers keep that order; unconstrained,
@@ -162,12 +168,12 @@ struct Tile {
       if constexpr (WHAT == 1) {
         if ((usemask >> r) & 1u) {
           if (store_lane) *reinterpret_cast<vecf*>(dst + off0 + r * pitch) = u[r];
-          if constexpr (RES == 1) acc(u[r], cur, store_lane, rc);
         }
-      } else if constexpr (WHAT == 2) {
-        if ((usemask >> r) & 1u) acc(u[r], cur, store_lane, rc);
       } else if constexpr (WHAT == 3) {
         sink->row(r, u[r], cur);
+      }
+      if constexpr (RES == 1) {
+        if (((usemask & resmask) >> r) & 1u) acc(u[r], cur, res_lane, res_cols);
       }
       prev = cur;
       if (i == R / 2 - 1) last_nb = xc.mid();

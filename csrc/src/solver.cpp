@@ -627,6 +627,8 @@ gpu::StencilGeom Solver::geom() const {
 
 int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
   if (!resident_ || plan[i].k != T_ || plan[i].rl != 0) return 0;
+  // A check may end a span (its residual taken in the last pass, at any
+  // step, on the device-judged path: replay_check re-runs the span).
   if (tr_->world() > 1 && !resident_force_ && device_users(P_.device >= 0 ? P_.device : 0) > 1)
     return 0;
   const int k = T_;
@@ -642,17 +644,18 @@ int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
                 blk_.ly + (blk_.nbr[East] >= 0 ? (ew ? round_down(gc - k, 4) : 0) : 0)};
   int n = 0;
   for (size_t j = i; j < plan.size(); ++j) {
-    if (plan[j].k != k || plan[j].rl != 0) break;
+    if (plan[j].k != k || (plan[j].rl != 0 && !gated())) break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
     if (ns) gr -= k;
     if (ew) gc = round_down(gc - k, 4);
     ++n;
+    if (plan[j].rl != 0) break;
   }
   if (n < 2 || !gpu::tb_resident_fits(box, k)) return 0;
   return n;
 }
 
-void Solver::enqueue_resident(int k, int n) {
+void Solver::enqueue_resident(int k, int n, int rl_last) {
   TraceRange trace("heat.resident");
   // The first pass's exchange (if its ghosts ran out) and box; the later
   // passes only shrink the ghost validity (resident_span checked that none
@@ -667,7 +670,8 @@ void Solver::enqueue_resident(int k, int n) {
   for (int j = 1; j < n; ++j) (void)ensure_ghosts(k, s_comp_);
   HEAT_CHECK(stat_exchanges_ - ex0 <= 1, "resident span of %d passes needs an exchange", n);
   const int cur0 = cur_;
-  const int out = cur_ ^ (n & 1);
+  // Always into the other buffer: the source stays intact for replay_check.
+  const int out = cur_ ^ 1;
   {
     PhaseScope phase(this, kCompute, s_comp_);
     gpu::TbResidentBuffers xb;
@@ -678,18 +682,34 @@ void Solver::enqueue_resident(int k, int n) {
     xb.flags = d_flags_;
     xb.max_tiles = int(kResidentFlagBytes / 4);
     xb.err = d_flags_ + kResidentFlagBytes / 4;
-    gpu::tb_resident_step(field_[cur_], field_[out], geom(), box, k, n, xb, s_comp_);
+    gpu::tb_resident_step(field_[cur_], field_[out], geom(), box, k, n, xb, s_comp_, -1,
+                          rl_last > 0 ? d_resid_ : nullptr, rl_last, blk_.lx, blk_.ly);
   }
   resident_used_ = true;
+  if (rl_last > 0) {
+    // The check ending the span (gated runs only: the judge zeroes the word).
+    TraceRange trace("heat.allreduce");
+    PhaseScope phase(this, kReduce, s_comp_);
+    if (tr_->device_memory() && tr_->world() > 1)
+      tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
+    gpu::judge_check(d_resid_, static_cast<gpu::DeviceGate*>(d_gate_), P_.eps,
+                     P_.compat == Compat::Mpi, s_comp_);
+    check_log_.push_back(step_ + int64_t(n - 1) * k + rl_last);
+  }
   for (int j = 0; j < n; ++j) {
     PassRec rec;
     rec.step0 = step_ + int64_t(j) * k;
     rec.k = k;
-    rec.rl = 0;
-    rec.cur0 = j == 0 ? cur0 : out;
+    rec.rl = j + 1 == n ? rl_last : 0;
+    rec.cur0 = j == 0 || j + 1 == n ? cur0 : out;
     rec.cur1 = out;
     rec.gr1 = gr_;
     rec.gc1 = gc_;
+    if (j + 1 == n) {
+      rec.span = n;
+      rec.er = ext.first;
+      rec.ec = ext.second;
+    }
     pass_log_.push_back(rec);
   }
   cur_ = out;
@@ -880,7 +900,7 @@ void Solver::enqueue_segment(const std::vector<PassPlan>& plan) {
   for (size_t i = 0; i < plan.size();) {
     const int n = on_gpu() ? resident_span(plan, i) : 0;
     if (n >= 2) {
-      enqueue_resident(plan[i].k, n);
+      enqueue_resident(plan[i].k, n, plan[i + size_t(n) - 1].rl);
       i += size_t(n);
     } else {
       enqueue_pass(plan[i].k, plan[i].rl);
@@ -1189,7 +1209,13 @@ void Solver::replay_check(const PassRec& p) {
   HEAT_CHECK(tb_kernel(), "replay of an inner-pass check needs the TB kernel");
   HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(unsigned), s_comp_));  // reopen: DeviceGate::stop
   cur_ = p.cur0;
-  compute_gpu(p.rl, 0, false, 0);
+  // A resident span: its first span - 1 passes over the span's (first) box,
+  // as the launch ran them, then the check's rl steps.
+  for (int j = 0; j + 1 < p.span; ++j) {
+    compute_gpu(p.k, 0, false, 0, 0, p.er, p.ec);
+    cur_ ^= 1;
+  }
+  compute_gpu(p.rl, 0, false, 0, 0, p.span > 1 ? p.er : 0, p.span > 1 ? p.ec : 0);
   cur_ ^= 1;
   gr_ = gc_ = 0;  // the replayed buffer's ghosts are stale
   sync_watch();

@@ -83,15 +83,53 @@ def test_resident_multirank_deep_halo(gpu, monkeypatch, world, kw):
 
 @pytest.mark.parametrize("interval", [50, 20, 7])
 def test_resident_with_checks(gpu, monkeypatch, interval):
-    # Checks are never inside a resident span (a check pass runs on its own,
-    # its residual possibly at an inner level); the spans between them stay
-    # resident.  Converges, bitwise vs the CPU oracle and vs separate passes.
+    # A check may END a resident span: its residual is taken in the launch's
+    # last pass (at an inner step or the last), over the owned block; a
+    # converging check replays the span from its source buffer.  Every 7
+    # steps two checks fall into one pass (cut passes, no span).  Converges,
+    # bitwise vs the CPU oracle and vs separate passes.
     cfg = HeatConfig(nx=48, ny=96, steps=40000, converge=True, check_interval=interval,
                      eps=1e-3, init="ref-wrap", backend="hip", tb_depth=12)
     g1, r1 = _solve(cfg, None, True, monkeypatch)
     g0, r0 = _solve(cfg, None, False, monkeypatch)
     c, rc = _solve(cfg.replace(backend="cpu", tb_depth=1), None, False, monkeypatch)
     assert r1[0].converged and r1[0].converged_at == rc[0].converged_at == r0[0].converged_at
-    if interval >= 2 * 12:
+    if interval >= 20:
         assert r1[0].resident_passes > 0
     assert np.array_equal(g1, c) and np.array_equal(g0, c)
+
+
+@pytest.mark.parametrize("world,kw,interval,check", [
+    (1, dict(nx=1024, ny=8192), 20, 4),               # step 80: level 8 of a 2-pass span
+    (1, dict(nx=1024, ny=8192), 60, 1),               # step 60: the last step of a 5-pass span
+    (1, dict(nx=1024, ny=8192), 50, 2),               # step 100: level 4 of a 4-pass span
+    (2, dict(nx=1024, ny=1024, decomp="rows"), 20, 4),  # deep halos: the owned rows only
+    (4, dict(nx=1024, ny=1024, px=2, py=2), 50, 1),     # 2-D blocks: owned rows and columns only
+])
+def test_resident_span_converges_inside(gpu, monkeypatch, world, kw, interval, check):
+    # eps just above the CPU oracle's residual at check `check`: the run
+    # converges exactly there, inside or at the end of a resident span, and
+    # its state is the span replayed from its source buffer.
+    base = HeatConfig(steps=0, converge=True, check_interval=interval, eps=0.0, init="random",
+                      seed=4, backend="cpu", tb_depth=1, nx=kw["nx"], ny=kw["ny"])
+    with HeatSolver(base) as c:
+        res = [np.float32(c.run(interval).last_resid) for _ in range(check)]
+        want = c.gather()
+    assert all(res[i] > res[i + 1] for i in range(len(res) - 1)), res
+    eps = float(np.nextafter(res[-1], np.float32(np.inf)))
+    cfg = HeatConfig(steps=0, converge=True, check_interval=interval, eps=eps, init="random",
+                     seed=4, backend="hip", tb_depth=12, **kw)
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "2" if world > 1 else "1")
+    if world == 1:
+        with HeatSolver(cfg) as s:
+            r = s.run(400)
+            got = s.gather()
+    else:
+        out = run_group(cfg, world, lambda s: (s.run(400), s.gather()))
+        r = out[0][0]
+        got = next(g for _, g in out if g is not None)
+        assert all(o[0].converged_at == r.converged_at for o in out)
+    assert r.resident_passes > 0, r
+    assert r.converged and r.converged_at == interval * check, (r.converged_at, res)
+    assert np.float32(r.last_resid) == res[-1]
+    assert np.array_equal(got, want), np.abs(got - want).max()
