@@ -46,12 +46,14 @@ $(BUILD)/obj/%.o: csrc/kernels/%.hip
 # two layouts of one struct (TbArgs).
 $(foreach o,$(OBJS),$(if $(wildcard $(o:.o=.d)),,$(eval $(o): $(HDRS) $(KHDRS))))
 
+# Linked under a temporary name and renamed: a copy of the tree taken while
+# a build runs holds the old library or the new one, never a partial file.
 $(LIBDIR)/libheat.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@.tmp $(OBJS) $(LDFLAGS) && mv -f $@.tmp $@
 
 $(BUILD)/heat: csrc/apps/heat_main.cpp $(OBJS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -x hip csrc/apps/heat_main.cpp -x none $(OBJS) -o $@ $(LDFLAGS)
+	$(HIPCC) $(HIPFLAGS) -x hip csrc/apps/heat_main.cpp -x none $(OBJS) -o $@.tmp $(LDFLAGS) && mv -f $@.tmp $@
 
 probe: $(BUILD)/overlap_probe
 $(BUILD)/overlap_probe: tools/overlap_probe.cpp $(OBJS) $(HDRS)

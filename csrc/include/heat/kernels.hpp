@@ -186,8 +186,9 @@ struct TbTuning {
   int tile_waves = 0;      // HEAT_TB_TILE_WAVES: waves per kTile workgroup, 8 or 16 (0: planner)
   int tile_xl = -1;        // HEAT_TB_TILE_XL: kTile lane shifts, 0 DPP, 1 ds_bpermute,
                            // 2 mixed (-1: mixed unless the variant has kTileDpp)
-  int res_diag = 0;        // HEAT_TB_RES_DIAG: resident-tile timing diagnostics (WRONG
-                           // results): bit 0 no neighbour wait, 1 no ghost reload, 2 no publish
+  int res_diag = 0;        // HEAT_TB_RES_DIAG: resident-tile timing diagnostics (bits 0-2
+                           // give WRONG results): bit 0 no neighbour wait, 1 no ghost reload,
+                           // 2 no publish; bit 3 every tile on the masked (edge) path
 };
 TbTuning tb_tuning();  // a copy of the current set
 void tb_set_tuning(const TbTuning& t);

@@ -62,8 +62,9 @@ struct ResArgs {
   unsigned* flags;      // one word per tile, zeroed before the launch
   unsigned* err;        // non-zero: a neighbour wait gave up (bounded spin)
   int64_t own_r1, own_c1;  // owned block [0, own_r1) x [0, own_c1): the residual's cells
-  int diag;             // timing diagnostics (HEAT_TB_RES_DIAG, wrong results):
-                        // bit 0 no neighbour wait, 1 no ghost reload, 2 no publish
+  int diag;             // timing diagnostics (HEAT_TB_RES_DIAG; bits 0-2 give wrong
+                        // results): bit 0 no neighbour wait, 1 no ghost reload, 2 no
+                        // publish, 3 every tile on the masked path
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
   const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
   const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
-  const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
+  const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2 &&
+                        !(ra.diag & 8);
   const float m = interior ? resident_run<R, NW, 0, XL, RES>(ra, bx, strip, t, blk, xch)
                            : resident_run<R, NW, 1, XL, RES>(ra, bx, strip, t, blk, xch);
   if constexpr (RES == 1) {
