@@ -133,22 +133,30 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // only their K-deep ghost rings between passes through two exchange fields
 // (same layout as the field) and per-tile flags.  The tiles of the box must
 // all be co-resident (tb_resident_fits).  src is read by the first pass only;
-// dst receives the last pass's box.  resid: the max |delta| of the LAST
-// pass's step res_level (1..depth; a check that ends the span) over the owned
-// block [0, own_rows) x [0, own_cols) only (nullptr: none).
+// dst receives the last pass's box.  checks: convergence checks inside the
+// launch (increasing passes, at most one per pass): check c writes the max
+// |delta| of step checks[c].step (1..depth) of pass checks[c].pass into
+// resids[c] (atomic max, words zeroed by the caller) over the owned block
+// [0, own_rows) x [0, own_cols) only.
 struct TbResidentBuffers {
   float* base[2] = {nullptr, nullptr};  // exchange field allocations
   int64_t origin = 0;                   // owned cell (0, 0) in floats from base
   int64_t bytes = 0;                    // allocation size
-  unsigned* flags = nullptr;            // >= max_tiles words, 16-byte aligned
+  unsigned* flags = nullptr;            // >= max_tiles words, 16-byte aligned, zeroed once
   int max_tiles = 0;
+  unsigned* done = nullptr;             // completion counter, zeroed once
   unsigned* err = nullptr;              // set non-zero if a neighbour wait gave up
 };
+struct TbResidentCheck {
+  int pass = 0, step = 0;
+};
+constexpr int kTbResidentMaxChecks = 32;
 bool tb_resident_fits(const Box& box, int depth, int variant = -1);
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                       int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,
-                      int variant = -1, unsigned* resid = nullptr, int res_level = 0,
-                      int64_t own_rows = 0, int64_t own_cols = 0);
+                      int variant = -1, const TbResidentCheck* checks = nullptr,
+                      int nchecks = 0, unsigned* resids = nullptr, int64_t own_rows = 0,
+                      int64_t own_cols = 0);
 
 // The automatic variant choice at this depth takes a residual at any inner
 // level (depth 12: level-split pipelines or workgroup tiles), so a
@@ -247,7 +255,10 @@ struct DeviceGate {
   unsigned last_bits;   // residual (float bits) of the last judged check
   unsigned pad[3];
 };
-void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st);
+// n > 1: the residual words resid[0..n) of n consecutive checks, judged in
+// order in one launch (the checks of a resident span).
+void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
+                 int n = 1);
 
 // Max |a-b| over a box (standalone residual), atomically into *resid.
 void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,

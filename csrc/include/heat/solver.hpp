@@ -70,6 +70,9 @@ class Solver {
 
   // Advance up to `steps` steps.  In converge mode, checks follow the
   // canonical/compat schedule and the call stops at the first converged check.
+  // A multi-rank run that throws aborts this rank's communicator first: its
+  // queued collectives would otherwise wait for peers forever (and the
+  // destructor's device syncs with them).
   RunStats run(int64_t steps);
   // Run the configured number of steps (Params::steps given at construction
   // by the caller; compat=mpi adds one).
@@ -136,8 +139,9 @@ class Solver {
     int k = 0, rl = 0;
     int cur0 = 0, cur1 = 0;
     int64_t gr1 = 0, gc1 = 0;
-    // A check that ends a resident span: the span's passes (cur0 = its
-    // source buffer) and box growth (er, ec), for replay_check.
+    // A pass of a resident span: its position in the span (span = passes
+    // from the span's start through this one; cur0 = the span's source
+    // buffer) and the span's box growth (er, ec), for replay_check.
     int span = 1;
     int64_t er = 0, ec = 0;
   };
@@ -157,11 +161,13 @@ class Solver {
   void enqueue_pass(int k, int rl);
   // Resident tiles: passes [i, i + n) of the plan in ONE launch whose tiles
   // stay in VGPRs (gpu::tb_resident_step).  resident_span returns n (0: not
-  // eligible): same depth, no check, no exchange after the first pass, and
-  // every tile of the first pass's box co-resident.
+  // eligible): same depth, no exchange after the first pass, a check only in
+  // the last pass (device-judged runs), and every tile of the first pass's
+  // box co-resident.
   int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
   static int device_users(int dev);  // live GPU solvers of this process on dev
-  void enqueue_resident(int k, int n, int rl_last);
+  void enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int n);
+  RunStats run_impl(int64_t steps);
   gpu::StencilGeom geom() const;
   void exchange(int buf, int k, hipStream_t st);
   // `st`: the stream to launch on (nullptr = the compute stream).

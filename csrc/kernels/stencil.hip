@@ -137,25 +137,29 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
   wave_max_atomic(m, resid);
 }
 
-__global__ void judge_kernel(unsigned* resid, DeviceGate* gate, double eps, int mpi_compat) {
+__global__ void judge_kernel(unsigned* resids, int n, DeviceGate* gate, double eps,
+                             int mpi_compat) {
   if (threadIdx.x != 0) return;
-  if (gate->stop == 0u) {
-    const unsigned bits = *resid;
-    float r;
-    __builtin_memcpy(&r, &bits, 4);
-    const unsigned ordinal = gate->checks;
-    gate->checks = ordinal + 1u;
-    gate->last_bits = bits;
-    unsigned why = 0u;
-    if ((bits & 0x7F800000u) == 0x7F800000u) why = 2u;  // inf or NaN
-    else if (mpi_compat ? double(r) <= eps : r < float(eps)) why = 1u;
-    if (why) {
-      gate->reason = why;
-      gate->stop_check = ordinal;
-      gate->stop = 1u;
+  // Checks in order: the first converging one closes the gate.
+  for (int i = 0; i < n; ++i) {
+    if (gate->stop == 0u) {
+      const unsigned bits = resids[i];
+      float r;
+      __builtin_memcpy(&r, &bits, 4);
+      const unsigned ordinal = gate->checks;
+      gate->checks = ordinal + 1u;
+      gate->last_bits = bits;
+      unsigned why = 0u;
+      if ((bits & 0x7F800000u) == 0x7F800000u) why = 2u;  // inf or NaN
+      else if (mpi_compat ? double(r) <= eps : r < float(eps)) why = 1u;
+      if (why) {
+        gate->reason = why;
+        gate->stop_check = ordinal;
+        gate->stop = 1u;
+      }
     }
+    resids[i] = 0u;
   }
-  *resid = 0u;
 }
 
 __device__ __forceinline__ int float_key(float f) {
@@ -789,8 +793,10 @@ void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, 
   HIP_CHECK(hipGetLastError());
 }
 
-void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st) {
-  hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, gate, eps, int(mpi_compat));
+void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
+                 int n) {
+  HEAT_CHECK(n >= 1, "judge of %d checks", n);
+  hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, n, gate, eps, int(mpi_compat));
   HIP_CHECK(hipGetLastError());
 }
 

@@ -52,6 +52,8 @@
 
 namespace heat::gpu::tbw {
 
+constexpr int kResMaxChecks = kTbResidentMaxChecks;
+
 struct ResArgs {
   TbArgs a;             // box[0]: the launch's box; src: pass 0 input; dst: last pass output
   int passes;           // P >= 2
@@ -59,9 +61,16 @@ struct ResArgs {
   float* xbase[2];      // exchange fields (allocation bases, same layout as the field)
   int64_t xorigin;      // owned cell (0, 0) in floats from an allocation base
   int xbytes;           // allocation size (buffer descriptor range, < 2^31)
-  unsigned* flags;      // one word per tile, zeroed before the launch
+  unsigned* flags;      // one word per tile, zero at launch (the previous launch's last
+                        // tile re-zeroes them, see tile_resident_kernel)
+  unsigned* done;       // tiles finished (zero at launch, re-zeroed with the flags)
   unsigned* err;        // non-zero: a neighbour wait gave up (bounded spin)
   int64_t own_r1, own_c1;  // owned block [0, own_r1) x [0, own_c1): the residual's cells
+  // Convergence checks inside the launch: check c takes the residual of
+  // step chk_step[c] (1..K) of pass chk_pass[c] into resids[c] (RES 1).
+  int nchk;
+  unsigned* resids;
+  int chk_pass[kResMaxChecks], chk_step[kResMaxChecks];
   int diag;             // timing diagnostics (HEAT_TB_RES_DIAG; bits 0-2 give wrong
                         // results): bit 0 no neighbour wait, 1 no ghost reload, 2 no
                         // publish, 3 every tile on the masked path
@@ -72,13 +81,32 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // Neighbour waits give up after this many polls (~0.3 s with s_sleep 2).
 constexpr unsigned kSpinLimit = 1u << 22;
 
-// RES 1: the residual of the LAST pass (a check that ends the span) at its
-// step a.res_level, under a uniform row mask that is zero in every other
-// step (tb_tile_core.hpp).  Returns this lane's max.  A separate
-// instantiation: the RES 0 kernel keeps its register allocation.
+// One max per workgroup into *word (a non-negative float's bits order like
+// the float; NaN has its sign cleared by fabs).  Every thread calls it.
+template <int NW>
+__device__ __forceinline__ void wg_max_atomic(float m, unsigned* word, unsigned* wmax) {
+  unsigned mm = __float_as_uint(m);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mm = max(mm, unsigned(__shfl_xor(int(mm), off)));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned r = 0u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r = max(r, wmax[i]);
+    atomicMax(word, r);
+  }
+  __syncthreads();  // wmax is reused by the next check
+}
+
+// RES 1: the residuals of the checks inside the launch (ResArgs::chk_*): a
+// check pass accumulates the max under a uniform row mask that is zero in
+// every other step (tb_tile_core.hpp), and the workgroup's max goes to its
+// word at the end of that pass.  A separate instantiation: the RES 0 kernel
+// keeps its register allocation.
 template <int R, int NW, int MODE, int XL, int RES>
-__device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
-                                             int u, vecf (*xch)[2][NW][64]) {
+__device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
+                                             int u, vecf (*xch)[2][NW][64], unsigned* wmax) {
   const TbArgs& a = ra.a;
   const int K = ra.depth;
   const int lane = threadIdx.x & 63;
@@ -120,7 +148,8 @@ __device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx
     const unsigned top = h >= 32 ? ~0u : (1u << h) - 1u;
     return l >= h ? 0u : top & ~((1u << l) - 1u);
   };
-  unsigned rowmask = MODE == 1 ? bits(1 - (g.gx0 + row0), g.nx - 1 - (g.gx0 + row0)) : ~0u;
+  unsigned rowmask;
+  tile_mode_setup(up, g, col, bits(1 - (g.gx0 + row0), g.nx - 1 - (g.gx0 + row0)), rowmask);
   unsigned usemask = bits(ub - row0, ue - row0);
   // Edge-band rows (published in full width) and ghost rows (reloaded in
   // full width): the K useful rows next to each useful-row boundary, and the
@@ -128,10 +157,6 @@ __device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx
   const unsigned bandmask = usemask & (bits(ub - row0, ub + K - row0) | bits(ue - K - row0, ue - row0));
   const unsigned ghostmask =
       bits(max(ub - K, bx.r0) - row0, ub - row0) | bits(ue - row0, min(ue + K, bx.r1) - row0);
-  if constexpr (MODE == 1) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) up.cm[j] = tbdetail::in_interior(g.gy0 + col + j, g.ny);
-  }
   // Lanes of the column bands: useful lanes within KK of the useful edge
   // (published in every useful row) and overlap lanes inside the box
   // (reloaded in every useful row).
@@ -191,7 +216,13 @@ __device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx
             nopub ? false : band_lane, vlane, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
-    const int rs = LAST && RES ? a.res_level - 1 : -1;
+    // The check of this pass (at most one), if any.
+    int ci = -1;
+    if constexpr (RES == 1) {
+      for (int c = 0; c < ra.nchk; ++c)
+        if (ra.chk_pass[c] == p) ci = c;
+    }
+    const int rs = ci >= 0 ? ra.chk_step[ci] - 1 : -1;
     auto xstep = [&](auto down_c, auto what_c, int s) {
       constexpr bool D = decltype(down_c)::value;
       xc.p = s & 1;
@@ -212,6 +243,12 @@ __device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx
     }
     xstep(Down{}, Plain{}, s);
     xstep(Up{}, std::integral_constant<int, LAST ? 1 : 3>{}, s + 1);
+    if constexpr (RES == 1) {
+      if (ci >= 0) {
+        wg_max_atomic<NW>(T.m, ra.resids + ci, wmax);
+        T.m = 0.f;
+      }
+    }
   };
 
   // Wait for the neighbours' pass p - 1 bands, then reload the ghost ring.
@@ -267,7 +304,6 @@ __device__ __forceinline__ float resident_run(const ResArgs& ra, const TbBox& bx
   }
   refill(P - 1);
   pass(std::true_type{}, P - 1);
-  return T.m;
 }
 
 template <int R, int NW, int XL, int RES>
@@ -289,26 +325,31 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t cbase = bx.c0 + int64_t(strip) * (256 - 2 * KK);
   const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
   const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
-  const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
-  const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2 &&
-                        !(ra.diag & 8);
-  const float m = interior ? resident_run<R, NW, 0, XL, RES>(ra, bx, strip, t, blk, xch)
-                           : resident_run<R, NW, 1, XL, RES>(ra, bx, strip, t, blk, xch);
-  if constexpr (RES == 1) {
-    // One atomic per workgroup (tb_tile.hip): non-negative floats (and NaN,
-    // sign cleared by fabs) order like their bit patterns.
-    __shared__ unsigned wmax[NW];
-    unsigned mm = __float_as_uint(m);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mm = max(mm, unsigned(__shfl_xor(int(mm), off)));
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mm;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned r = 0u;
-#pragma unroll
-      for (int i = 0; i < NW; ++i) r = max(r, wmax[i]);
-      atomicMax(a.resid, r);
-    }
+  // This wave's global rows (the mode is per wave, see tile_mode).
+  const int64_t wx_lo = g.gx0 + ub - K + int64_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * R;
+  const int64_t wx_hi = wx_lo + R - 1;
+  const int mode = (ra.diag & 8) ? kTileGeneric : tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi);
+  __shared__ unsigned wmax[NW];
+  tile_dispatch<XL>(mode, [&](auto mode_c) {
+    resident_run<R, NW, decltype(mode_c)::value, XL, RES>(ra, bx, strip, t, blk, xch, wmax);
+    return 0.f;
+  });
+  // Completion: the tile that finishes last (every other tile is past its
+  // last flag poll) re-zeroes the flags and the counter for the next launch
+  // on this stream, in place of a memset node per launch (~5 us each, as much
+  // as a check's whole judge launch).  A gated launch returns above without
+  // touching either.
+  __shared__ unsigned last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned n = __hip_atomic_fetch_add(ra.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = n + 1 == unsigned(gridDim.x);
+  }
+  __syncthreads();
+  if (last) {
+    for (int i = threadIdx.x; i < int(gridDim.x); i += blockDim.x)
+      __hip_atomic_store(ra.flags + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(ra.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -381,12 +422,16 @@ struct ResPlan {
 };
 
 int res_xl(int variant, const TbTuning& tune) {
-  return tune.tile_xl >= 0 && tune.tile_xl <= 2 ? tune.tile_xl : (variant & tbv::kTileDpp) ? 0 : 2;
+  // Mixed lane shifts unless a forced variant asks for DPP (variant -1 is the
+  // automatic choice, not "every flag": it ran the all-DPP build, 11 % slower
+  // than ds_bpermute shifts on 1024 x 8192, profiles/r4_resident.md).
+  if (tune.tile_xl >= 0 && tune.tile_xl <= 2) return tune.tile_xl;
+  return variant >= 0 && (variant & tbv::kTileDpp) ? 0 : 2;
 }
 
-// The shape with the fewest rows per SIMD among those whose tiles are all
-// co-resident (one dispatch round; the occupancy of the resident
-// instantiation itself, bounded by its VGPR granule).
+// The shape with the lowest step estimate (tile_step_estimate) among those
+// whose tiles are all co-resident (one dispatch round; the occupancy of the
+// resident instantiation itself, bounded by its VGPR granule).
 ResPlan plan_res(const Box& box, int depth, int xl, const TbTuning& tune) {
   ResPlan best;
   if (box.empty() || depth < 4 || depth % 2 != 0 || box.c0 % 4 != 0) return best;
@@ -405,10 +450,7 @@ ResPlan plan_res(const Box& box, int depth, int xl, const TbTuning& tune) {
     const int64_t units = ceil_div(box.cols(), W) * ceil_div(box.rows(), hmax);
     const int occ = cached_occupancy_res(sh.rows, sh.waves, xl);
     if (occ <= 0 || units > int64_t(cus) * occ) continue;
-    const int per_simd = occ * sh.waves / 4;
-    // Work per step: rows per SIMD of the resident waves (x 2.7 cycles per op
-    // with two or more workgroups per CU, 3.1 with one; tb_tile.hip).
-    const double est = double(per_simd) * sh.rows * (occ >= 2 ? 2.7 : 3.1);
+    const double est = tile_step_estimate(units, cus, occ, sh.rows, sh.waves);
     if (best.rows == 0 || est < best_est) {
       best_est = est;
       best = ResPlan{sh.rows, sh.waves, int(units)};
@@ -437,8 +479,8 @@ bool tb_resident_fits(const Box& box, int depth, int variant) {
 
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                       int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,
-                      int variant, unsigned* resid, int res_level, int64_t own_rows,
-                      int64_t own_cols) {
+                      int variant, const TbResidentCheck* checks, int nchecks, unsigned* resids,
+                      int64_t own_rows, int64_t own_cols) {
   using namespace tbw;
   HEAT_CHECK(passes >= 2, "a resident launch spans >= 2 passes (%d)", passes);
   const TbTuning tune = tb_tuning();
@@ -455,10 +497,20 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   TbArgs& a = ra.a;
   a.src = src;
   a.dst = dst;
-  HEAT_CHECK(resid == nullptr || (res_level >= 1 && res_level <= depth),
-             "resident residual at step %d of a depth-%d pass", res_level, depth);
-  a.resid = resid;
-  a.res_level = resid ? res_level : depth;
+  HEAT_CHECK(nchecks >= 0 && nchecks <= kResMaxChecks && (nchecks == 0 || resids != nullptr),
+             "%d checks in a resident launch (at most %d)", nchecks, kResMaxChecks);
+  for (int c = 0; c < nchecks; ++c) {
+    HEAT_CHECK(checks[c].pass >= 0 && checks[c].pass < passes && checks[c].step >= 1 &&
+                   checks[c].step <= depth && (c == 0 || checks[c].pass > checks[c - 1].pass),
+               "resident check %d at pass %d step %d (passes %d, depth %d)", c, checks[c].pass,
+               checks[c].step, passes, depth);
+    ra.chk_pass[c] = checks[c].pass;
+    ra.chk_step[c] = checks[c].step;
+  }
+  ra.nchk = nchecks;
+  ra.resids = resids;
+  a.resid = nchecks > 0 ? resids : nullptr;  // selects the RES 1 instantiation
+  a.res_level = depth;
   a.g = g;
   a.flags = (variant < 0 || (variant & tbv::kXcdGroups)) ? tbdetail::kTbXcdGroups : 0;
   TbBox& t = a.box[0];
@@ -480,13 +532,15 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   ra.xbase[1] = xb.base[1];
   ra.xorigin = xb.origin;
   ra.xbytes = int(xb.bytes);
+  HEAT_CHECK(xb.done != nullptr, "resident launch without a completion counter");
   ra.flags = xb.flags;
+  ra.done = xb.done;
   ra.err = xb.err;
-  ra.own_r1 = resid ? own_rows : box.r1;
-  ra.own_c1 = resid ? own_cols : box.c1;
+  ra.own_r1 = nchecks > 0 ? own_rows : box.r1;
+  ra.own_c1 = nchecks > 0 ? own_cols : box.c1;
   ra.diag = tune.res_diag;
-  // Re-initialise every call: the flags (a memset node under capture).
-  HIP_CHECK(hipMemsetAsync(xb.flags, 0, size_t(round_up(int64_t(pl.units) * 4, 16)), st));
+  // The flags and the completion counter are zero: zeroed once when the
+  // buffers are allocated, then by the last tile of every launch.
   if (const char* e = std::getenv("HEAT_TB_TRACE"); e && *e && *e != '0') {
     static std::mutex mu;
     static std::set<std::string> seen;

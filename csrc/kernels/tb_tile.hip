@@ -92,12 +92,9 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
     const unsigned top = h >= 32 ? ~0u : (1u << h) - 1u;
     return l >= h ? 0u : top & ~((1u << l) - 1u);
   };
-  unsigned rowmask = MODE == 1 ? bits(1 - (g.gx0 + row0), g.nx - 1 - (g.gx0 + row0)) : ~0u;
+  unsigned rowmask;
+  tile_mode_setup(up, g, col, bits(1 - (g.gx0 + row0), g.nx - 1 - (g.gx0 + row0)), rowmask);
   unsigned usemask = bits(ub - row0, ue - row0);
-  if constexpr (MODE == 1) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) up.cm[j] = tbdetail::in_interior(g.gy0 + col + j, g.ny);
-  }
   int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last step stores)
   opaque(off0);
   const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
@@ -163,15 +160,17 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int u = blk - bx.wave_begin;
   const int strip = u / bx.nchunks, t = u % bx.nchunks;
   const StencilGeom& g = a.g;
-  // Tile-uniform Dirichlet mode (every wave of the block takes the same path).
+  // Dirichlet mode: per wave (tile_mode), the same steps and barriers on every path.
   const int KK = (K + 3) & ~3;
   const int64_t cbase = bx.c0 + int64_t(strip) * (256 - 2 * KK);
   const int64_t gy_lo = g.gy0 + cbase - KK, gy_hi = gy_lo + 255;
   const int64_t ub = bx.r0 + int64_t(t) * bx.chunk_len;
-  const int64_t gx_lo = g.gx0 + ub - K, gx_hi = gx_lo + int64_t(NW) * R - 1;
-  const bool interior = gx_lo >= 1 && gx_hi <= g.nx - 2 && gy_lo >= 1 && gy_hi <= g.ny - 2;
-  const float m = interior ? tile_run<R, NW, 0, RES, XL>(a, bx, strip, t, K, xch)
-                           : tile_run<R, NW, 1, RES, XL>(a, bx, strip, t, K, xch);
+  // This wave's global rows (the mode is per wave, see tile_mode).
+  const int64_t wx_lo = g.gx0 + ub - K + int64_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * R;
+  const int64_t wx_hi = wx_lo + R - 1;
+  const float m = tile_dispatch<XL>(tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi), [&](auto mode_c) {
+    return tile_run<R, NW, decltype(mode_c)::value, RES, XL>(a, bx, strip, t, K, xch);
+  });
   if constexpr (RES == 1) {
     // One atomic per workgroup: a per-wave atomicMax on the one residual
     // word from ~4000 waves serialised at the memory side (~37 us per check
@@ -312,9 +311,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
       if (!boxes[b].empty()) units += ceil_div(boxes[b].cols(), W) * ceil_div(boxes[b].rows(), hmax);
     const int occ = cached_occupancy(sh.rows, sh.waves, bp);
     if (occ <= 0) continue;
-    const int per_simd = occ * sh.waves / 4;  // resident waves per SIMD
-    const int64_t rounds = ceil_div(units, int64_t(cus) * occ);
-    const double est = double(rounds) * per_simd * sh.rows * (occ >= 2 ? 2.7 : 3.1);
+    const double est = tile_step_estimate(units, cus, occ, sh.rows, sh.waves);
     if (best.rows == 0 || est < best_est) {
       best_est = est;
       best = sh;

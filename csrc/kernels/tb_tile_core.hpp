@@ -72,8 +72,25 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// MODE 0: no cell of the tile is on the plate's fixed ring (or outside it);
-// MODE 1: per-lane column masks and a per-row (uniform) mask keep those cells.
+// Dirichlet handling of one WAVE of a tile (wave-uniform: the waves of a
+// tile run the same steps and barriers, each on its own path).  Cells outside
+// the plate are don't-care (their values only flow further out); only the
+// fixed ring must be kept.
+//   kTileInterior   none of the wave's rows is a plate edge row and no column
+//                   of the tile is a plate edge column (rows outside the plate
+//                   are computed like any other: don't-care);
+//   kTileGeneric    per-lane column masks AND a per-row (uniform) mask: the
+//                   wave holds plate row 0 or nx-1 (or the tile both edge
+//                   columns);
+//   kTileLeft       plate column 0 is element 0 of one lane: one v_cndmask
+//                   per row;
+//   kTileRight + e  plate column ny-1 is element e of one lane.
+// Edge waves set the pace (a tile waits at every step's barrier for its
+// slowest wave, a resident grid for its slowest tile): the generic path
+// issues ~36 % more instructions per step than the interior, the column
+// modes ~3 % (profiles/r4_resident.md).
+constexpr int kTileInterior = 0, kTileGeneric = 1, kTileLeft = 3, kTileRight = 4;
+
 template <int MODE, int XL>
 struct Upd {
   float cx, cy;
@@ -91,15 +108,69 @@ struct Upd {
       // the DPP build folds it into v_add_f32_dpp.
       r[j] = j == 3 ? stencil(b[j], a[j], c[j], e, w, cx, cy) : stencil(b[j], a[j], c[j], w, e, cx, cy);
     }
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == kTileGeneric) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] = (cm[j] && row_ok) ? r[j] : b[j];
+    } else if constexpr (MODE == kTileLeft) {
+      r[0] = cm[0] ? b[0] : r[0];  // cm[0]: this lane holds plate column 0
+    } else if constexpr (MODE >= kTileRight) {
+      r[MODE - kTileRight] = cm[0] ? b[MODE - kTileRight] : r[MODE - kTileRight];
     }
     return r;
   }
 };
 
 struct TileNoSink;
+
+// A wave's mode from its global rows [wx_lo, wx_hi] and the tile's global
+// columns [gy_lo, gy_hi].  Lanes hold 4 columns starting at a global column
+// = gy0 (mod 4).
+__device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, int64_t wx_hi,
+                                         int64_t gy_lo, int64_t gy_hi) {
+  const bool edge_row = (wx_lo <= 0 && 0 <= wx_hi) || (wx_lo <= g.nx - 1 && g.nx - 1 <= wx_hi);
+  const bool left = gy_lo < 1, right = gy_hi > g.ny - 2;
+  if (edge_row || (left && right)) return kTileGeneric;
+  if (!left && !right) return kTileInterior;
+  if (left) return (g.gy0 & 3) == 0 ? kTileLeft : kTileGeneric;
+  return kTileRight + int((g.ny - 1 - g.gy0) & 3);
+}
+
+// Calls f(std::integral_constant<int, MODE>) for the tile's mode.  The edge
+// modes are built for the default lane shifts (XL 2) only; the others take
+// the generic path on every edge tile.
+template <int XL, class F>
+__device__ __forceinline__ float tile_dispatch(int mode, F&& f) {
+  using std::integral_constant;
+  if (mode == kTileInterior) return f(integral_constant<int, kTileInterior>{});
+  if constexpr (XL == 2) {
+    switch (mode) {
+      case kTileLeft: return f(integral_constant<int, kTileLeft>{});
+      case kTileRight + 0: return f(integral_constant<int, kTileRight + 0>{});
+      case kTileRight + 1: return f(integral_constant<int, kTileRight + 1>{});
+      case kTileRight + 2: return f(integral_constant<int, kTileRight + 2>{});
+      case kTileRight + 3: return f(integral_constant<int, kTileRight + 3>{});
+      default: break;
+    }
+  }
+  return f(integral_constant<int, kTileGeneric>{});
+}
+
+// Mode-dependent setup of an Upd and the tile's row mask (rows row0 + r,
+// r < R, that are global interior rows).
+template <int MODE, int XL>
+__device__ __forceinline__ void tile_mode_setup(Upd<MODE, XL>& up, const StencilGeom& g,
+                                                int64_t col, unsigned interior_rows,
+                                                unsigned& rowmask) {
+  rowmask = MODE == kTileGeneric ? interior_rows : ~0u;
+  if constexpr (MODE == kTileGeneric) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) up.cm[j] = tbdetail::in_interior(g.gy0 + col + j, g.ny);
+  } else if constexpr (MODE == kTileLeft) {
+    up.cm[0] = g.gy0 + col == 0;
+  } else if constexpr (MODE >= kTileRight) {
+    up.cm[0] = g.gy0 + col + (MODE - kTileRight) == g.ny - 1;
+  }
+}
 
 // RES: 0 no residual; 1 max |new - old| over the rows of `resmask` (a
 // runtime mask: zero except in the step that takes the check's residual,

@@ -180,12 +180,15 @@ void Solver::alloc() {
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
-    HIP_CHECK(hipMalloc(&d_resid_, 256));
+    HIP_CHECK(hipMalloc(&d_resid_, 256));  // 64 words: the checks of a resident span
+    HIP_CHECK(hipMemset(d_resid_, 0, 256));
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
     if (resident_) {
       for (auto& b : xbase_) HIP_CHECK(hipMalloc(&b, size_t(L_.bytes())));
+      // Flags, then the error word and the completion counter: zeroed once
+      // here, then by the last tile of every launch (tb_resident.hip).
       HIP_CHECK(hipMalloc(&d_flags_, kResidentFlagBytes + 256));
       HIP_CHECK(hipMemset(d_flags_, 0, kResidentFlagBytes + 256));
       HIP_CHECK(hipHostMalloc(&h_err_, 256));
@@ -626,36 +629,39 @@ gpu::StencilGeom Solver::geom() const {
 }
 
 int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
-  if (!resident_ || plan[i].k != T_ || plan[i].rl != 0) return 0;
-  // A check may end a span (its residual taken in the last pass, at any
-  // step, on the device-judged path: replay_check re-runs the span).
+  if (!resident_ || plan[i].k != T_) return 0;
+  // Checks may fall in any pass of a span (one per pass, device-judged runs:
+  // each residual goes to its own word, judged in order after the launch;
+  // replay_check re-runs the span up to a converging one).
   if (tr_->world() > 1 && !resident_force_ && device_users(P_.device >= 0 ? P_.device : 0) > 1)
     return 0;
   const int k = T_;
   const bool ns = cart_.px > 1, ew = cart_.py > 1;
   // Ghost validity after the first pass's (possible) exchange, then the
   // bookkeeping of ensure_ghosts pass by pass: the span ends before a pass
-  // that would need an exchange, or a check.
+  // that would need an exchange.
   int64_t gr = gr_, gc = gc_;
   if ((ns && gr < k) || (ew && gc < k)) gr = gc = H_;
   const Box box{blk_.nbr[North] >= 0 ? -(ns ? gr - k : 0) : 0,
                 blk_.lx + (blk_.nbr[South] >= 0 ? (ns ? gr - k : 0) : 0),
                 blk_.nbr[West] >= 0 ? -(ew ? round_down(gc - k, 4) : 0) : 0,
                 blk_.ly + (blk_.nbr[East] >= 0 ? (ew ? round_down(gc - k, 4) : 0) : 0)};
-  int n = 0;
+  int n = 0, nchk = 0;
   for (size_t j = i; j < plan.size(); ++j) {
-    if (plan[j].k != k || (plan[j].rl != 0 && !gated())) break;
+    if (plan[j].k != k) break;
+    if (plan[j].rl != 0 && (!gated() || nchk == gpu::kTbResidentMaxChecks)) break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
     if (ns) gr -= k;
     if (ew) gc = round_down(gc - k, 4);
     ++n;
-    if (plan[j].rl != 0) break;
+    if (plan[j].rl != 0) ++nchk;
   }
   if (n < 2 || !gpu::tb_resident_fits(box, k)) return 0;
   return n;
 }
 
-void Solver::enqueue_resident(int k, int n, int rl_last) {
+void Solver::enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int n) {
+  const int k = plan[i0].k;
   TraceRange trace("heat.resident");
   // The first pass's exchange (if its ghosts ran out) and box; the later
   // passes only shrink the ghost validity (resident_span checked that none
@@ -672,6 +678,9 @@ void Solver::enqueue_resident(int k, int n, int rl_last) {
   const int cur0 = cur_;
   // Always into the other buffer: the source stays intact for replay_check.
   const int out = cur_ ^ 1;
+  std::vector<gpu::TbResidentCheck> chk;
+  for (int j = 0; j < n; ++j)
+    if (plan[i0 + size_t(j)].rl > 0) chk.push_back({j, plan[i0 + size_t(j)].rl});
   {
     PhaseScope phase(this, kCompute, s_comp_);
     gpu::TbResidentBuffers xb;
@@ -682,34 +691,36 @@ void Solver::enqueue_resident(int k, int n, int rl_last) {
     xb.flags = d_flags_;
     xb.max_tiles = int(kResidentFlagBytes / 4);
     xb.err = d_flags_ + kResidentFlagBytes / 4;
+    xb.done = xb.err + 1;
     gpu::tb_resident_step(field_[cur_], field_[out], geom(), box, k, n, xb, s_comp_, -1,
-                          rl_last > 0 ? d_resid_ : nullptr, rl_last, blk_.lx, blk_.ly);
+                          chk.data(), int(chk.size()), d_resid_, blk_.lx, blk_.ly);
   }
   resident_used_ = true;
-  if (rl_last > 0) {
-    // The check ending the span (gated runs only: the judge zeroes the word).
+  if (!chk.empty()) {
+    // The span's checks (gated runs only: the judge zeroes the words), one
+    // all-reduce and one judge launch for all of them.
     TraceRange trace("heat.allreduce");
     PhaseScope phase(this, kReduce, s_comp_);
     if (tr_->device_memory() && tr_->world() > 1)
-      tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), 1, s_comp_);
+      tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), int(chk.size()), s_comp_);
     gpu::judge_check(d_resid_, static_cast<gpu::DeviceGate*>(d_gate_), P_.eps,
-                     P_.compat == Compat::Mpi, s_comp_);
-    check_log_.push_back(step_ + int64_t(n - 1) * k + rl_last);
+                     P_.compat == Compat::Mpi, s_comp_, int(chk.size()));
+    for (const auto& c : chk) check_log_.push_back(step_ + int64_t(c.pass) * k + c.step);
   }
   for (int j = 0; j < n; ++j) {
+    // Intermediate states live only in registers: a check's pass records the
+    // span's source and its offset in the span (replay_check re-runs it).
     PassRec rec;
     rec.step0 = step_ + int64_t(j) * k;
     rec.k = k;
-    rec.rl = j + 1 == n ? rl_last : 0;
-    rec.cur0 = j == 0 || j + 1 == n ? cur0 : out;
-    rec.cur1 = out;
+    rec.rl = plan[i0 + size_t(j)].rl;
+    rec.cur0 = cur0;
+    rec.cur1 = j + 1 == n ? out : -1;  // only the last pass's state is in memory
     rec.gr1 = gr_;
     rec.gc1 = gc_;
-    if (j + 1 == n) {
-      rec.span = n;
-      rec.er = ext.first;
-      rec.ec = ext.second;
-    }
+    rec.span = j + 1;
+    rec.er = ext.first;
+    rec.ec = ext.second;
     pass_log_.push_back(rec);
   }
   cur_ = out;
@@ -900,7 +911,7 @@ void Solver::enqueue_segment(const std::vector<PassPlan>& plan) {
   for (size_t i = 0; i < plan.size();) {
     const int n = on_gpu() ? resident_span(plan, i) : 0;
     if (n >= 2) {
-      enqueue_resident(plan[i].k, n, plan[i + size_t(n) - 1].rl);
+      enqueue_resident(plan, i, n);
       i += size_t(n);
     } else {
       enqueue_pass(plan[i].k, plan[i].rl);
@@ -1182,7 +1193,7 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   // first rl steps replayed from its (untouched) source buffer.  Restored
   // before a non-finite residual is reported too, so gather() / save() after
   // the error see the check's state, as on the host-judged path.
-  if (p->rl == p->k) {
+  if (p->rl == p->k && p->cur1 >= 0) {
     cur_ = p->cur1;
     gr_ = p->gr1;
     gc_ = p->gc1;
@@ -1222,6 +1233,24 @@ void Solver::replay_check(const PassRec& p) {
 }
 
 RunStats Solver::run(int64_t steps) {
+  try {
+    return run_impl(steps);
+  } catch (...) {
+    if (tr_->world() > 1) {
+      if (capturing_) {
+        // Drop the half-built capture (its stream is unusable otherwise).
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(s_comp_, &g);
+        if (g) (void)hipGraphDestroy(g);
+        capturing_ = false;
+      }
+      abort();
+    }
+    throw;
+  }
+}
+
+RunStats Solver::run_impl(int64_t steps) {
   TraceRange trace("heat.run");
   RunStats s;
   HEAT_CHECK(steps >= 0, "negative step count");
