@@ -223,26 +223,17 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
         if (ra.chk_pass[c] == p) ci = c;
     }
     const int rs = ci >= 0 ? ra.chk_step[ci] - 1 : -1;
-    auto xstep = [&](auto down_c, auto what_c, int s) {
+    tile_pass_steps<RES == 1, LAST ? 1 : 3>(K, rs, [&](auto down_c, auto what_c, auto acc_c, int s) {
       constexpr bool D = decltype(down_c)::value;
       xc.p = s & 1;
       xc.last_w = xc.next_w = D ? wb : wa;
       const vecf first_nb = xc.efirst;
       opaque(rowmask);
       opaque(usemask);
-      unsigned rm = s == rs ? resmask : 0u;
-      opaque(rm);
-      T.template step<D, decltype(what_c)::value>(first_nb, xc, up, rowmask, usemask, store_lane,
-                                                   rc, dst + lo, off0, pitch, &pub, rm, res_rc);
-    };
-    using Plain = std::integral_constant<int, 0>;
-    int s = 0;
-    for (; s + 2 < K; s += 2) {
-      xstep(Down{}, Plain{}, s);
-      xstep(Up{}, Plain{}, s + 1);
-    }
-    xstep(Down{}, Plain{}, s);
-    xstep(Up{}, std::integral_constant<int, LAST ? 1 : 3>{}, s + 1);
+      T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
+          first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub, resmask,
+          res_rc);
+    });
     if constexpr (RES == 1) {
       if (ci >= 0) {
         wg_max_atomic<NW>(T.m, ra.resids + ci, wmax);

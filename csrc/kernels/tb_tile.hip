@@ -105,9 +105,9 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   xch[1][1][w][lane] = T.u[0];
   lds_barrier();
   xc.efirst = xch[1][0][wa][lane];
-  // RES 1: the residual of step res_level - 1 (uniform mask, zero elsewhere).
+  // RES 1: the residual of step res_level - 1 (tile_pass_steps).
   const int rs = RES ? a.res_level - 1 : -1;
-  auto xstep = [&](auto down_c, auto last_c, int s) {
+  tile_pass_steps<RES == 1, 1>(K, rs, [&](auto down_c, auto what_c, auto acc_c, int s) {
     constexpr bool D = decltype(down_c)::value;
     xc.p = s & 1;
     // Down: the last row needs the wave below; so does the next (up) step's first.
@@ -115,24 +115,9 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
     const vecf first_nb = xc.efirst;
     opaque(rowmask);
     opaque(usemask);
-    unsigned rm = s == rs ? ~0u : 0u;
-    opaque(rm);
-    T.template step<D, decltype(last_c)::value>(first_nb, xc, up, rowmask, usemask, store_lane, rc,
-                                                 dst + lo, off0, pitch,
-                                                 static_cast<TileNoSink*>(nullptr), rm);
-  };
-  using Down = std::true_type;
-  using Up = std::false_type;
-  using Plain = std::integral_constant<int, 0>;
-  using Last = std::integral_constant<int, 1>;
-  // Steps in (down, up) pairs (K is even, see launch()).
-  int s = 0;
-  for (; s + 2 < K; s += 2) {
-    xstep(Down{}, Plain{}, s);
-    xstep(Up{}, Plain{}, s + 1);
-  }
-  xstep(Down{}, Plain{}, s);
-  xstep(Up{}, Last{}, s + 1);
+    T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
+        first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch);
+  });
   return T.m;
 }
 

@@ -135,6 +135,57 @@ __device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, in
   return kTileRight + int((g.ny - 1 - g.gy0) & 3);
 }
 
+// The K steps of a pass (K even) as (down, up) pairs, the last step's body
+// LAST_WHAT: st(down_c, what_c, acc_c, s) for s = 0..K-1.  With RES, step rs
+// (0..K-1; < 0: none) takes the residual: the pass runs plain pairs up to
+// the pair holding rs, that pair (the accumulating step its own body), then
+// plain pairs again -- loops free of per-step branches (a uniform branch
+// choosing the body in every step made the allocator spill 250-870 B/lane).
+template <bool RES, int LAST_WHAT, class StepFn>
+__device__ __forceinline__ void tile_pass_steps(int K, int rs, StepFn&& st) {
+  using Down = std::true_type;
+  using Up = std::false_type;
+  using Plain = std::integral_constant<int, 0>;
+  using Last = std::integral_constant<int, LAST_WHAT>;
+  using Acc = std::true_type;
+  using No = std::false_type;
+  int s = 0;
+  if constexpr (RES) {
+    if (rs >= 0 && rs < K - 2) {
+      for (; s + 2 <= rs; s += 2) {
+        st(Down{}, Plain{}, No{}, s);
+        st(Up{}, Plain{}, No{}, s + 1);
+      }
+      if (s == rs) {
+        st(Down{}, Plain{}, Acc{}, s);
+        st(Up{}, Plain{}, No{}, s + 1);
+      } else {
+        st(Down{}, Plain{}, No{}, s);
+        st(Up{}, Plain{}, Acc{}, s + 1);
+      }
+      s += 2;
+    }
+  }
+  for (; s + 2 < K; s += 2) {
+    st(Down{}, Plain{}, No{}, s);
+    st(Up{}, Plain{}, No{}, s + 1);
+  }
+  if constexpr (RES) {
+    if (rs == K - 2) {
+      st(Down{}, Plain{}, Acc{}, s);
+      st(Up{}, Last{}, No{}, s + 1);
+      return;
+    }
+    if (rs == K - 1) {
+      st(Down{}, Plain{}, No{}, s);
+      st(Up{}, Last{}, Acc{}, s + 1);
+      return;
+    }
+  }
+  st(Down{}, Plain{}, No{}, s);
+  st(Up{}, Last{}, No{}, s + 1);
+}
+
 // Calls f(std::integral_constant<int, MODE>) for the tile's mode.  The edge
 // modes are built for the default lane shifts (XL 2) only; the others take
 // the generic path on every edge tile.
@@ -172,9 +223,10 @@ __device__ __forceinline__ void tile_mode_setup(Upd<MODE, XL>& up, const Stencil
   }
 }
 
-// RES: 0 no residual; 1 max |new - old| over the rows of `resmask` (a
-// runtime mask: zero except in the step that takes the check's residual,
-// TbArgs::res_level, the last step or an inner one of a full-depth pass).
+// RES 1: the instantiation that takes residuals; the step that takes one is
+// its own body (step<.., ACC = true>: max |new - old| over the useful rows
+// in `resmask`), so the other steps carry no residual code (a per-row
+// branch in every step split the rows into basic blocks: 13 % slower).
 template <int R, int MODE, int RES, int XL>
 struct Tile {
   vecf u[R];
@@ -192,9 +244,9 @@ struct Tile {
   // WHAT 1 (LAST): the launch's last step stores every useful row as soon as
   // it is computed (dst + off0 + r * pitch, this lane's columns if
   // store_lane); WHAT 3: every row goes to sink->row(r, new, old) (the
-  // resident kernel's edge-band publish, tb_resident.hip).  With RES 1 any
-  // step accumulates max |new - old| over the useful rows in resmask.
-  template <bool DOWN, int WHAT, class Xc, class Sink = TileNoSink>
+  // resident kernel's edge-band publish, tb_resident.hip).  ACC: this step
+  // accumulates max |new - old| over the useful rows in resmask.
+  template <bool DOWN, int WHAT, bool ACC = false, class Xc, class Sink = TileNoSink>
   __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, XL>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
                                        float* __restrict__ dst, int64_t off0, int64_t pitch,
@@ -243,7 +295,7 @@ struct Tile {
       } else if constexpr (WHAT == 3) {
         sink->row(r, u[r], cur);
       }
-      if constexpr (RES == 1) {
+      if constexpr (ACC) {
         if (((usemask & resmask) >> r) & 1u) acc(u[r], cur, res_lane, res_cols);
       }
       prev = cur;

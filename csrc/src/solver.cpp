@@ -1237,6 +1237,7 @@ RunStats Solver::run(int64_t steps) {
     return run_impl(steps);
   } catch (...) {
     if (tr_->world() > 1) {
+      std::fprintf(stderr, "[heat] rank %d: run failed; aborting the communicator\n", tr_->rank());
       if (capturing_) {
         // Drop the half-built capture (its stream is unusable otherwise).
         hipGraph_t g = nullptr;
@@ -1245,6 +1246,7 @@ RunStats Solver::run(int64_t steps) {
         capturing_ = false;
       }
       abort();
+      std::fprintf(stderr, "[heat] rank %d: communicator aborted\n", tr_->rank());
     }
     throw;
   }

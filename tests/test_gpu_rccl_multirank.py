@@ -119,14 +119,23 @@ def test_rccl_dead_peer_fails_fast(gpu, tmp_path):
         procs.append(subprocess.Popen(cmd, env=env, cwd=tmp_path, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     t0 = time.time()
+    outs = [None, None]
     try:
-        out1, err1 = procs[1].communicate(timeout=60)
-        out0, err0 = procs[0].communicate(timeout=60)
+        outs[1] = procs[1].communicate(timeout=60)
+        outs[0] = procs[0].communicate(timeout=60)
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        tails = [p.communicate()[1][-1500:] for p in procs]
+        pytest.fail(f"rank(s) still running after 60 s; rank 0 stderr: {tails[0]!r}; "
+                    f"rank 1 stderr: {tails[1]!r}")
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+    (out0, err0), (out1, err1) = outs
     elapsed = time.time() - t0
     assert procs[1].returncode != 0 and "injected transport failure" in err1, err1[-2000:]
     assert procs[0].returncode != 0, (out0[-500:], err0[-2000:])
