@@ -33,6 +33,8 @@ $(BUILD)/obj/%.o: csrc/src/%.cpp
 
 KHDRS    := $(wildcard csrc/kernels/*.hpp csrc/kernels/*.inl)
 $(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o $(BUILD)/obj/tb_resident.o \
+  $(BUILD)/obj/tb_tile_xl0.o $(BUILD)/obj/tb_tile_xl1.o $(BUILD)/obj/tb_tile_xl2.o \
+  $(BUILD)/obj/tb_resident_xl0.o $(BUILD)/obj/tb_resident_xl1.o $(BUILD)/obj/tb_resident_xl2.o \
   $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o \
   $(BUILD)/obj/tb_split_mixed.o: HIPFLAGS += -fno-slp-vectorize
 

@@ -134,10 +134,10 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // (same layout as the field) and per-tile flags.  The tiles of the box must
 // all be co-resident (tb_resident_fits).  src is read by the first pass only;
 // dst receives the last pass's box.  checks: convergence checks inside the
-// launch (increasing passes, at most one per pass): check c writes the max
-// |delta| of step checks[c].step (1..depth) of pass checks[c].pass into
-// resids[c] (atomic max, words zeroed by the caller) over the owned block
-// [0, own_rows) x [0, own_cols) only.
+// launch (increasing passes, at most one per pass, each at the pass's last
+// step: checks[c].step == depth): check c writes the max |delta| of that
+// step into resids[c] (atomic max, words zeroed by the caller) over the
+// owned block [0, own_rows) x [0, own_cols) only.
 struct TbResidentBuffers {
   float* base[2] = {nullptr, nullptr};  // exchange field allocations
   int64_t origin = 0;                   // owned cell (0, 0) in floats from base

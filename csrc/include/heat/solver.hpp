@@ -152,6 +152,7 @@ class Solver {
   // Every rank's depth-T launches are small enough for the workgroup-tile
   // kernel (even depths): remainder passes are then split into even parts.
   bool tile_sized() const;
+  bool tile_sized_at(int depth) const;
   // Passes for steps [step0, step0+n), cut at every check point (the
   // residual is the last level of its pass).
   std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;
@@ -260,6 +261,7 @@ class Solver {
   // Key: (steps, check phase or -1, cur, ghost rows, ghost cols).
   std::map<std::tuple<int64_t, int64_t, int, int64_t, int64_t>, GraphEntry> graphs_;
   bool capturing_ = false;
+  std::atomic<bool> rccl_graphs_{false};  // a live graph captured RCCL calls (abort())
   // Gated runs: the device gate, two pinned host copies (one per segment
   // parity) and their events; the pass log of the segment being enqueued.
   void* d_gate_ = nullptr;

@@ -470,7 +470,6 @@ bool tb_mid_residual(int depth) {
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
              int res_level) {
-  HEAT_CHECK(tb_depth_supported(depth), "unsupported TB depth %d", depth);
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   HEAT_CHECK(res_level >= 0 && res_level <= depth, "residual level %d of a depth-%d pass",
              res_level, depth);
@@ -485,6 +484,12 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       if (!boxes[b].empty()) rows4 += ceil_div(boxes[b].cols(), W4) * boxes[b].rows();
     variant = tb_auto_variant(depth, rows4 / tb_simd_count());
   }
+  // The tile kernel takes any even depth up to 16 (Solver picks 10 for
+  // checks every 10k steps on tile-sized blocks); the streaming kernels the
+  // built ones.
+  const bool tile_depth = (variant & tbv::kTile) && depth % 2 == 0 && depth <= 16;
+  HEAT_CHECK(tb_depth_supported(depth) || tile_depth, "unsupported TB depth %d (variant %d)", depth,
+             variant);
   if (variant & tbv::kTile) {
     // The tile kernel runs steps in (down, up) pairs: even depths only; an
     // odd pass (a remainder or a check-cut pass) streams.

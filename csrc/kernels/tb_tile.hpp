@@ -8,6 +8,13 @@ namespace heat::gpu::tbw {  // workgroup tiles, rows of the tile in VGPRs (tb_ti
 bool launch(const tbdetail::TbArgs& args, int depth, int rows, int waves, bool bpermute,
             hipStream_t st);
 int occupancy(int rows, int waves, bool bpermute);  // resident blocks per CU (0: not built)
+// The lane-shift builds (tb_tile_xl<XL>.hip, compiled in parallel).
+bool tile_launch_x0(const tbdetail::TbArgs& args, int depth, int rows, int waves, hipStream_t st);
+bool tile_launch_x1(const tbdetail::TbArgs& args, int depth, int rows, int waves, hipStream_t st);
+bool tile_launch_x2(const tbdetail::TbArgs& args, int depth, int rows, int waves, hipStream_t st);
+int tile_occupancy_x0(int rows, int waves);
+int tile_occupancy_x1(int rows, int waves);
+int tile_occupancy_x2(int rows, int waves);
 // A kTile launch of tb_step (even depth): plans the tiles and launches.
 // res_level: the step (1..depth) whose residual goes to resid (0 = depth).
 void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox, int depth,

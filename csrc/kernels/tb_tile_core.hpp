@@ -136,54 +136,36 @@ __device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, in
 }
 
 // The K steps of a pass (K even) as (down, up) pairs, the last step's body
-// LAST_WHAT: st(down_c, what_c, acc_c, s) for s = 0..K-1.  With RES, step rs
-// (0..K-1; < 0: none) takes the residual: the pass runs plain pairs up to
-// the pair holding rs, that pair (the accumulating step its own body), then
-// plain pairs again -- loops free of per-step branches (a uniform branch
-// choosing the body in every step made the allocator spill 250-870 B/lane).
-template <bool RES, int LAST_WHAT, class StepFn>
-__device__ __forceinline__ void tile_pass_steps(int K, int rs, StepFn&& st) {
+// LAST_WHAT: st(down_c, what_c, acc_c, s) for s = 0..K-1.
+//   ACC_MODE 0: no residual anywhere;
+//   ACC_MODE 1: every step is the accumulating body (acc_c true) and the
+//     caller's per-step row mask picks the check's step (a per-row branch in
+//     every step: ~16 % slower per pass; the tile kernel's check passes);
+//   ACC_MODE 2: only the last step can accumulate, chosen per pass by
+//     acc_last (the resident kernel: its spans take checks at pass ends; the
+//     plain steps stay free of residual code, and one junction per pass
+//     keeps the allocation spill-free -- a body per check step spilled
+//     80-240 B/lane and ran 10 % slower).
+template <int ACC_MODE, int LAST_WHAT, class StepFn>
+__device__ __forceinline__ void tile_pass_steps(int K, bool acc_last, StepFn&& st) {
   using Down = std::true_type;
   using Up = std::false_type;
   using Plain = std::integral_constant<int, 0>;
   using Last = std::integral_constant<int, LAST_WHAT>;
-  using Acc = std::true_type;
-  using No = std::false_type;
+  using A = std::integral_constant<bool, ACC_MODE == 1>;
   int s = 0;
-  if constexpr (RES) {
-    if (rs >= 0 && rs < K - 2) {
-      for (; s + 2 <= rs; s += 2) {
-        st(Down{}, Plain{}, No{}, s);
-        st(Up{}, Plain{}, No{}, s + 1);
-      }
-      if (s == rs) {
-        st(Down{}, Plain{}, Acc{}, s);
-        st(Up{}, Plain{}, No{}, s + 1);
-      } else {
-        st(Down{}, Plain{}, No{}, s);
-        st(Up{}, Plain{}, Acc{}, s + 1);
-      }
-      s += 2;
-    }
-  }
   for (; s + 2 < K; s += 2) {
-    st(Down{}, Plain{}, No{}, s);
-    st(Up{}, Plain{}, No{}, s + 1);
+    st(Down{}, Plain{}, A{}, s);
+    st(Up{}, Plain{}, A{}, s + 1);
   }
-  if constexpr (RES) {
-    if (rs == K - 2) {
-      st(Down{}, Plain{}, Acc{}, s);
-      st(Up{}, Last{}, No{}, s + 1);
-      return;
-    }
-    if (rs == K - 1) {
-      st(Down{}, Plain{}, No{}, s);
-      st(Up{}, Last{}, Acc{}, s + 1);
+  st(Down{}, Plain{}, A{}, s);
+  if constexpr (ACC_MODE == 2) {
+    if (acc_last) {
+      st(Up{}, Last{}, std::true_type{}, s + 1);
       return;
     }
   }
-  st(Down{}, Plain{}, No{}, s);
-  st(Up{}, Last{}, No{}, s + 1);
+  st(Up{}, Last{}, A{}, s + 1);
 }
 
 // Calls f(std::integral_constant<int, MODE>) for the tile's mode.  The edge

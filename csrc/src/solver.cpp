@@ -318,15 +318,28 @@ int Solver::auto_tb_depth() const {
   if (!gpu::tb_variant_deep(gpu::tb_default_variant(gpu::kTbDeepDepth))) return 8;
   int64_t min_lx = INT64_MAX;
   for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
-  return min_lx >= 1024 ? gpu::kTbDeepDepth : 8;
+  const int base = min_lx >= 1024 ? gpu::kTbDeepDepth : 8;
+  // Convergence checks every C steps on tile-sized blocks: a depth that
+  // divides C puts every check at the end of a pass, where resident spans
+  // take it without leaving the launch (tb_resident.hip; a check inside a
+  // pass ends the span).  10 for C = 20, 50, 100, ...: 1024 x 8192 checking
+  // every 20 steps ran -21 % with its checks inside depth-12 passes.
+  if (P_.converge && P_.compat != Compat::Cuda && P_.check_interval % base != 0 &&
+      env_int("HEAT_TB_RESIDENT", 1) != 0) {
+    for (int d : {10, 8})
+      if (P_.check_interval % d == 0 && tile_sized_at(d)) return d;
+  }
+  return base;
 }
 
-bool Solver::tile_sized() const {
+bool Solver::tile_sized() const { return tile_sized_at(T_); }
+
+bool Solver::tile_sized_at(int depth) const {
   // The same rule as gpu::tb_auto_variant (strip-rows per SIMD of the owned
   // block), decided from the largest block of any rank so that every rank
   // plans the same passes.
   if (!on_gpu() || !tb_kernel()) return false;
-  const int64_t W = gpu::tb_strip_width(T_, 4), simds = gpu::tb_simd_count();
+  const int64_t W = gpu::tb_strip_width(depth, 4), simds = gpu::tb_simd_count();
   for (int r = 0; r < cart_.world; ++r) {
     const Block b = make_block(cart_, r, P_.nx, P_.ny);
     if (ceil_div(b.ly, W) * b.lx >= 64 * simds) return false;
@@ -630,9 +643,9 @@ gpu::StencilGeom Solver::geom() const {
 
 int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
   if (!resident_ || plan[i].k != T_) return 0;
-  // Checks may fall in any pass of a span (one per pass, device-judged runs:
-  // each residual goes to its own word, judged in order after the launch;
-  // replay_check re-runs the span up to a converging one).
+  // Checks may end any pass of a span (device-judged runs: each residual goes
+  // to its own word, judged in order after the launch; replay_check re-runs
+  // the span up to a converging one).
   if (tr_->world() > 1 && !resident_force_ && device_users(P_.device >= 0 ? P_.device : 0) > 1)
     return 0;
   const int k = T_;
@@ -649,7 +662,9 @@ int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
   int n = 0, nchk = 0;
   for (size_t j = i; j < plan.size(); ++j) {
     if (plan[j].k != k) break;
-    if (plan[j].rl != 0 && (!gated() || nchk == gpu::kTbResidentMaxChecks)) break;
+    // Checks at pass ends only (the resident kernel's residual step).
+    if (plan[j].rl != 0 && (!gated() || plan[j].rl != k || nchk == gpu::kTbResidentMaxChecks))
+      break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
     if (ns) gr -= k;
     if (ew) gc = round_down(gc - k, 4);
@@ -1052,14 +1067,18 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
       enqueue_segment(plan);
     } catch (...) {
       capturing_ = false;
-      hipGraph_t g2;
+      hipGraph_t g2 = nullptr;
       (void)hipStreamEndCapture(s_comp_, &g2);
+      // Release it now: a captured RCCL call holds a reference on the
+      // communicator until its graph is destroyed (ncclCommAbort waits).
+      if (g2) (void)hipGraphDestroy(g2);
       throw;
     }
     capturing_ = false;
     HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
     GraphEntry e;
     HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+    if (tr_->world() > 1 && tr_->device_memory()) rccl_graphs_ = true;
     HIP_CHECK(hipGraphDestroy(graph));
     e.cur_after = cur_;
     e.gr_after = gr_;
@@ -1237,7 +1256,7 @@ RunStats Solver::run(int64_t steps) {
     return run_impl(steps);
   } catch (...) {
     if (tr_->world() > 1) {
-      std::fprintf(stderr, "[heat] rank %d: run failed; aborting the communicator\n", tr_->rank());
+      std::fprintf(stderr, "[heat] rank %d: run failed; aborting\n", tr_->rank());
       if (capturing_) {
         // Drop the half-built capture (its stream is unusable otherwise).
         hipGraph_t g = nullptr;
@@ -1246,7 +1265,8 @@ RunStats Solver::run(int64_t steps) {
         capturing_ = false;
       }
       abort();
-      std::fprintf(stderr, "[heat] rank %d: communicator aborted\n", tr_->rank());
+      std::fprintf(stderr, "[heat] rank %d: aborted%s\n", tr_->rank(),
+                   rccl_graphs_.load() ? " (communicator left to process exit: live graphs)" : "");
     }
     throw;
   }
@@ -1361,7 +1381,12 @@ void Solver::sync_watch() {
 }
 
 void Solver::abort() {
-  if (!aborted_.exchange(true)) tr_->abort();
+  // ncclCommAbort waits until every graph that captured an RCCL call is
+  // destroyed; such a graph may still be running (waiting for the dead peer)
+  // and cannot be destroyed from here.  Then only mark the solver aborted:
+  // its waits throw, and the caller ends the process (the CLI exits without
+  // destructors; the peers' watchdogs end theirs).
+  if (!aborted_.exchange(true) && !rccl_graphs_.load()) tr_->abort();
 }
 
 void Solver::synchronize() {

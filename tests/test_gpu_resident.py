@@ -83,13 +83,13 @@ def test_resident_multirank_deep_halo(gpu, monkeypatch, world, kw):
 
 @pytest.mark.parametrize("interval", [50, 20, 7])
 def test_resident_with_checks(gpu, monkeypatch, interval):
-    # A check may END a resident span: its residual is taken in the launch's
-    # last pass (at an inner step or the last), over the owned block; a
-    # converging check replays the span from its source buffer.  Every 7
-    # steps two checks fall into one pass (cut passes, no span).  Converges,
-    # bitwise vs the CPU oracle and vs separate passes.
+    # Checks at pass ends ride inside resident spans (the automatic depth
+    # divides the interval: 10 for 20 and 50); a converging check replays the
+    # span from its source buffer.  Every 7 steps the checks fall inside
+    # passes (depth 8: cut passes, no spans).  Converges, bitwise vs the CPU
+    # oracle and vs separate passes.
     cfg = HeatConfig(nx=48, ny=96, steps=40000, converge=True, check_interval=interval,
-                     eps=1e-3, init="ref-wrap", backend="hip", tb_depth=12)
+                     eps=1e-3, init="ref-wrap", backend="hip")
     g1, r1 = _solve(cfg, None, True, monkeypatch)
     g0, r0 = _solve(cfg, None, False, monkeypatch)
     c, rc = _solve(cfg.replace(backend="cpu", tb_depth=1), None, False, monkeypatch)
@@ -100,9 +100,9 @@ def test_resident_with_checks(gpu, monkeypatch, interval):
 
 
 @pytest.mark.parametrize("world,kw,interval,check", [
-    (1, dict(nx=1024, ny=8192), 20, 4),               # step 80: level 8 of a 2-pass span
-    (1, dict(nx=1024, ny=8192), 60, 1),               # step 60: the last step of a 5-pass span
-    (1, dict(nx=1024, ny=8192), 50, 2),               # step 100: level 4 of a 4-pass span
+    (1, dict(nx=1024, ny=8192), 20, 4),               # depth 10: step 80 ends pass 8 of a span
+    (1, dict(nx=1024, ny=8192), 60, 1),               # depth 12: step 60 ends pass 5
+    (1, dict(nx=1024, ny=8192), 50, 2),               # depth 10: step 100
     (2, dict(nx=1024, ny=1024, decomp="rows"), 20, 4),  # deep halos: the owned rows only
     (4, dict(nx=1024, ny=1024, px=2, py=2), 50, 1),     # 2-D blocks: owned rows and columns only
 ])
@@ -118,7 +118,7 @@ def test_resident_span_converges_inside(gpu, monkeypatch, world, kw, interval, c
     assert all(res[i] > res[i + 1] for i in range(len(res) - 1)), res
     eps = float(np.nextafter(res[-1], np.float32(np.inf)))
     cfg = HeatConfig(steps=0, converge=True, check_interval=interval, eps=eps, init="random",
-                     seed=4, backend="hip", tb_depth=12, **kw)
+                     seed=4, backend="hip", **kw)
     monkeypatch.setenv("HEAT_TB_RESIDENT", "2" if world > 1 else "1")
     if world == 1:
         with HeatSolver(cfg) as s:
