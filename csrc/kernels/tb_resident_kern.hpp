@@ -180,8 +180,10 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       for (int c = 0; c < ra.nchk; ++c)
         if (ra.chk_pass[c] == p) ci = c;
     }
-    tile_pass_steps<RES == 1 ? 2 : 0, LAST ? 1 : 3>(K, ci >= 0, [&](auto down_c, auto what_c,
-                                                                    auto acc_c, int s) {
+    unsigned rm = ci >= 0 ? resmask : 0u;  // the last step's residual rows
+    opaque(rm);
+    tile_pass_steps<RES == 1 ? 2 : 0, LAST ? 1 : 3>(K, [&](auto down_c, auto what_c, auto acc_c,
+                                                          int s) {
       constexpr bool D = decltype(down_c)::value;
       xc.p = s & 1;
       xc.last_w = xc.next_w = D ? wb : wa;
@@ -189,7 +191,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       opaque(rowmask);
       opaque(usemask);
       T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-          first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub, resmask,
+          first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub, rm,
           res_rc);
     });
     if constexpr (RES == 1) {

@@ -141,31 +141,26 @@ __device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, in
 //   ACC_MODE 1: every step is the accumulating body (acc_c true) and the
 //     caller's per-step row mask picks the check's step (a per-row branch in
 //     every step: ~16 % slower per pass; the tile kernel's check passes);
-//   ACC_MODE 2: only the last step can accumulate, chosen per pass by
-//     acc_last (the resident kernel: its spans take checks at pass ends; the
-//     plain steps stay free of residual code, and one junction per pass
-//     keeps the allocation spill-free -- a body per check step spilled
-//     80-240 B/lane and ran 10 % slower).
+//   ACC_MODE 2: only the last step is the accumulating body, its row mask
+//     zero unless the pass ends at a check (the resident kernel: its spans
+//     take checks at pass ends; the other steps stay free of residual code).
+//     Choosing between two last-step bodies per pass, or a body per check
+//     step, spilled 80-330 B/lane.
 template <int ACC_MODE, int LAST_WHAT, class StepFn>
-__device__ __forceinline__ void tile_pass_steps(int K, bool acc_last, StepFn&& st) {
+__device__ __forceinline__ void tile_pass_steps(int K, StepFn&& st) {
   using Down = std::true_type;
   using Up = std::false_type;
   using Plain = std::integral_constant<int, 0>;
   using Last = std::integral_constant<int, LAST_WHAT>;
   using A = std::integral_constant<bool, ACC_MODE == 1>;
+  using AL = std::integral_constant<bool, ACC_MODE != 0>;
   int s = 0;
   for (; s + 2 < K; s += 2) {
     st(Down{}, Plain{}, A{}, s);
     st(Up{}, Plain{}, A{}, s + 1);
   }
   st(Down{}, Plain{}, A{}, s);
-  if constexpr (ACC_MODE == 2) {
-    if (acc_last) {
-      st(Up{}, Last{}, std::true_type{}, s + 1);
-      return;
-    }
-  }
-  st(Up{}, Last{}, A{}, s + 1);
+  st(Up{}, Last{}, AL{}, s + 1);
 }
 
 // Calls f(std::integral_constant<int, MODE>) for the tile's mode.  The edge

@@ -76,7 +76,7 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   // RES 1: the residual of step res_level - 1: a uniform row mask, zero in
   // every other step (tile_pass_steps ACC_MODE 1).
   const int rs = RES ? a.res_level - 1 : -1;
-  tile_pass_steps<RES == 1 ? 1 : 0, 1>(K, false, [&](auto down_c, auto what_c, auto acc_c, int s) {
+  tile_pass_steps<RES == 1 ? 1 : 0, 1>(K, [&](auto down_c, auto what_c, auto acc_c, int s) {
     constexpr bool D = decltype(down_c)::value;
     xc.p = s & 1;
     // Down: the last row needs the wave below; so does the next (up) step's first.

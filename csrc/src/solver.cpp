@@ -69,7 +69,9 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
     } else {
       T_ = P_.tb_depth > 0 ? P_.tb_depth : env_int("HEAT_TB_DEPTH", 0);
       if (T_ == 0) T_ = auto_tb_depth();
-      HEAT_CHECK(gpu::tb_depth_supported(T_), "TB depth %d not supported", T_);
+      HEAT_CHECK(gpu::tb_depth_supported(T_) || (T_ % 2 == 0 && T_ <= 16 && tile_sized_at(T_)),
+                 "TB depth %d not supported (1-8 and 12; even depths up to 16 on blocks small "
+                 "enough for the workgroup-tile kernel)", T_);
     }
   } else {
     HEAT_CHECK(!tr_->device_memory(), "transport %s needs the GPU backend", tr_->name());
