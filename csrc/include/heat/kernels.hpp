@@ -136,8 +136,10 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // dst receives the last pass's box.  checks: convergence checks inside the
 // launch (increasing passes, at most one per pass, each at the pass's last
 // step: checks[c].step == depth): check c writes the max |delta| of that
-// step into resids[c] (atomic max, words zeroed by the caller) over the
-// owned block [0, own_rows) x [0, own_cols) only.
+// step over the owned block [0, own_rows) x [0, own_cols) into
+// resids[slot * kTbResidentMaxChecks + c] (atomic max, tile t's slot t % 8;
+// words zeroed by the caller, kTbResidentSlots * kTbResidentMaxChecks of
+// them: judge_check(resids, ..., n, kTbResidentSlots, kTbResidentMaxChecks)).
 struct TbResidentBuffers {
   float* base[2] = {nullptr, nullptr};  // exchange field allocations
   int64_t origin = 0;                   // owned cell (0, 0) in floats from base
@@ -194,6 +196,8 @@ struct TbTuning {
   int tile_waves = 0;      // HEAT_TB_TILE_WAVES: waves per kTile workgroup, 8 or 16 (0: planner)
   int tile_xl = -1;        // HEAT_TB_TILE_XL: kTile lane shifts, 0 DPP, 1 ds_bpermute,
                            // 2 mixed (-1: mixed unless the variant has kTileDpp)
+  int tile_max_srps = 64;  // HEAT_TB_TILE_MAX: workgroup tiles below this many strip-rows
+                           // per SIMD (the automatic variant and Solver::tile_sized)
   int res_diag = 0;        // HEAT_TB_RES_DIAG: resident-tile timing diagnostics (bits 0-2
                            // give WRONG results): bit 0 no neighbour wait, 1 no ghost reload,
                            // 2 no publish; bit 3 every tile on the masked (edge) path
@@ -255,10 +259,15 @@ struct DeviceGate {
   unsigned last_bits;   // residual (float bits) of the last judged check
   unsigned pad[3];
 };
-// n > 1: the residual words resid[0..n) of n consecutive checks, judged in
-// order in one launch (the checks of a resident span).
+// n > 1: n consecutive checks judged in order in one launch (the checks of a
+// resident span); check i's residual is the max of resid[s * stride + i]
+// over s < slots (the span's tiles spread their atomics over `slots` cache
+// lines: 500 workgroups on one word serialised ~3.5 us per check).
 void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
-                 int n = 1);
+                 int n = 1, int slots = 1, int stride = 0);
+// The resident span's residual block: kTbResidentSlots lines of
+// kTbResidentMaxChecks words (TbResidentBuffers / tb_resident_step resids).
+constexpr int kTbResidentSlots = 8;
 
 // Max |a-b| over a box (standalone residual), atomically into *resid.
 void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,

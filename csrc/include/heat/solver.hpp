@@ -237,6 +237,9 @@ class Solver {
   // Host staging (staged_ mode), one pair per message of an exchange.
   static constexpr int kMaxMsgs = 8;
   static constexpr size_t kResidentFlagBytes = 16384;  // flags of up to 4096 resident tiles
+  static constexpr size_t kResidSpanOffset = 64;      // words: a resident span's residual block
+  static constexpr size_t kResidBytes =
+      4 * (kResidSpanOffset + size_t(gpu::kTbResidentSlots) * gpu::kTbResidentMaxChecks);
   float* stage_send_[kMaxMsgs] = {};
   float* stage_recv_[kMaxMsgs] = {};
   size_t stage_bytes_ = 0;

@@ -78,6 +78,11 @@ class Transport {
   // runtime, so there a peer waits for that runtime's own timeout (gloo's,
   // bounded in bench.py by its watchdog).
   virtual void abort() {}
+  // Give up without ncclCommAbort / ncclCommDestroy: both wait until every
+  // graph that captured a call of the communicator is destroyed, and such a
+  // graph may still be running, waiting for a dead peer.  The communicator
+  // and its resources are left to process exit.
+  virtual void abandon() {}
   virtual const char* name() const = 0;
   virtual TransportInfo info() const {
     TransportInfo t;

@@ -137,13 +137,17 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
   wave_max_atomic(m, resid);
 }
 
-__global__ void judge_kernel(unsigned* resids, int n, DeviceGate* gate, double eps,
-                             int mpi_compat) {
+__global__ void judge_kernel(unsigned* resids, int n, int slots, int stride, DeviceGate* gate,
+                             double eps, int mpi_compat) {
   if (threadIdx.x != 0) return;
   // Checks in order: the first converging one closes the gate.
   for (int i = 0; i < n; ++i) {
+    unsigned bits = 0u;
+    for (int s = 0; s < slots; ++s) {  // non-negative floats order like their bits
+      bits = max(bits, resids[s * stride + i]);
+      resids[s * stride + i] = 0u;
+    }
     if (gate->stop == 0u) {
-      const unsigned bits = resids[i];
       float r;
       __builtin_memcpy(&r, &bits, 4);
       const unsigned ordinal = gate->checks;
@@ -158,7 +162,6 @@ __global__ void judge_kernel(unsigned* resids, int n, DeviceGate* gate, double e
         gate->stop = 1u;
       }
     }
-    resids[i] = 0u;
   }
 }
 
@@ -281,6 +284,7 @@ TbTuning tuning_from_env() {
   t.tile_waves = std::max(0, geti("HEAT_TB_TILE_WAVES", 0));
   t.tile_xl = geti("HEAT_TB_TILE_XL", -1);
   t.res_diag = geti("HEAT_TB_RES_DIAG", 0) & 15;
+  t.tile_max_srps = std::max(0, geti("HEAT_TB_TILE_MAX", 64));
   if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);
   if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
     for (const char* q = e; *q;) {
@@ -411,7 +415,8 @@ int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
   // reports) at 36 and 54, where one wave per chunk loses 8 % inside the
   // plate (profiles/r3_tile.md).  Even depths only (the tile runs steps in
   // pairs).  From 64 the split pipelines keep the edge ranks within 2 %.
-  if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < 64) return tbv::kTile | tbv::kXcdGroups;
+  if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < tb_tuning().tile_max_srps)
+    return tbv::kTile | tbv::kXcdGroups;
   if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
   return tb_default_variant(depth);
 }
@@ -799,9 +804,11 @@ void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, 
 }
 
 void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
-                 int n) {
-  HEAT_CHECK(n >= 1, "judge of %d checks", n);
-  hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, n, gate, eps, int(mpi_compat));
+                 int n, int slots, int stride) {
+  HEAT_CHECK(n >= 1 && slots >= 1 && (slots == 1 || stride >= n), "judge of %d checks x %d slots",
+             n, slots);
+  hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, n, slots, stride, gate, eps,
+                     int(mpi_compat));
   HIP_CHECK(hipGetLastError());
 }
 

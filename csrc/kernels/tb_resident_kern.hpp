@@ -196,7 +196,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     });
     if constexpr (RES == 1) {
       if (ci >= 0) {
-        wg_max_atomic<NW>(T.m, ra.resids + ci, wmax);
+        wg_max_atomic<NW>(T.m, ra.resids + (u & (kTbResidentSlots - 1)) * kResMaxChecks + ci, wmax);
         T.m = 0.f;
       }
     }

@@ -182,8 +182,10 @@ void Solver::alloc() {
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
-    HIP_CHECK(hipMalloc(&d_resid_, 256));  // 64 words: the checks of a resident span
-    HIP_CHECK(hipMemset(d_resid_, 0, 256));
+    // Word 0: a pass's residual; from kResidSpanOffset: the residual block of
+    // a resident span's checks (slots x checks words).
+    HIP_CHECK(hipMalloc(&d_resid_, kResidBytes));
+    HIP_CHECK(hipMemset(d_resid_, 0, kResidBytes));
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
@@ -344,7 +346,7 @@ bool Solver::tile_sized_at(int depth) const {
   const int64_t W = gpu::tb_strip_width(depth, 4), simds = gpu::tb_simd_count();
   for (int r = 0; r < cart_.world; ++r) {
     const Block b = make_block(cart_, r, P_.nx, P_.ny);
-    if (ceil_div(b.ly, W) * b.lx >= 64 * simds) return false;
+    if (ceil_div(b.ly, W) * b.lx >= int64_t(gpu::tb_tuning().tile_max_srps) * simds) return false;
   }
   return true;
 }
@@ -710,7 +712,8 @@ void Solver::enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int 
     xb.err = d_flags_ + kResidentFlagBytes / 4;
     xb.done = xb.err + 1;
     gpu::tb_resident_step(field_[cur_], field_[out], geom(), box, k, n, xb, s_comp_, -1,
-                          chk.data(), int(chk.size()), d_resid_, blk_.lx, blk_.ly);
+                          chk.data(), int(chk.size()), d_resid_ + kResidSpanOffset, blk_.lx,
+                          blk_.ly);
   }
   resident_used_ = true;
   if (!chk.empty()) {
@@ -718,10 +721,12 @@ void Solver::enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int 
     // all-reduce and one judge launch for all of them.
     TraceRange trace("heat.allreduce");
     PhaseScope phase(this, kReduce, s_comp_);
+    unsigned* rs = d_resid_ + kResidSpanOffset;
     if (tr_->device_memory() && tr_->world() > 1)
-      tr_->allreduce_max(reinterpret_cast<float*>(d_resid_), int(chk.size()), s_comp_);
-    gpu::judge_check(d_resid_, static_cast<gpu::DeviceGate*>(d_gate_), P_.eps,
-                     P_.compat == Compat::Mpi, s_comp_, int(chk.size()));
+      tr_->allreduce_max(reinterpret_cast<float*>(rs),
+                         gpu::kTbResidentSlots * gpu::kTbResidentMaxChecks, s_comp_);
+    gpu::judge_check(rs, static_cast<gpu::DeviceGate*>(d_gate_), P_.eps, P_.compat == Compat::Mpi,
+                     s_comp_, int(chk.size()), gpu::kTbResidentSlots, gpu::kTbResidentMaxChecks);
     for (const auto& c : chk) check_log_.push_back(step_ + int64_t(c.pass) * k + c.step);
   }
   for (int j = 0; j < n; ++j) {
@@ -1388,7 +1393,9 @@ void Solver::abort() {
   // and cannot be destroyed from here.  Then only mark the solver aborted:
   // its waits throw, and the caller ends the process (the CLI exits without
   // destructors; the peers' watchdogs end theirs).
-  if (!aborted_.exchange(true) && !rccl_graphs_.load()) tr_->abort();
+  if (aborted_.exchange(true)) return;
+  if (rccl_graphs_.load()) tr_->abandon();
+  else tr_->abort();
 }
 
 void Solver::synchronize() {

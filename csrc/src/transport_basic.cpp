@@ -95,6 +95,7 @@ class FaultTransport final : public Transport {
   void barrier() override { in_->barrier(); }
   void check() override { in_->check(); }
   void abort() override { in_->abort(); }
+  void abandon() override { in_->abandon(); }
   const char* name() const override { return in_->name(); }
   TransportInfo info() const override { return in_->info(); }
 

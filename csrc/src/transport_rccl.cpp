@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -39,10 +40,12 @@ class RcclTransport final : public Transport {
     HIP_CHECK(hipMalloc(&scratch_, 64));
   }
   ~RcclTransport() override {
+    if (abandoned_) return;
     if (scratch_) (void)hipFree(scratch_);
     std::lock_guard<std::mutex> lk(mu_);
     if (comm_) (void)ncclCommDestroy(comm_);
   }
+  void abandon() override { abandoned_ = true; }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   bool device_memory() const override { return true; }
@@ -125,6 +128,7 @@ class RcclTransport final : public Transport {
   }
   int rank_, world_;
   mutable std::mutex mu_;
+  std::atomic<bool> abandoned_{false};
   ncclComm_t comm_ = nullptr;
   float* scratch_ = nullptr;
 };

@@ -46,15 +46,15 @@ XGMI = {
 # (plate edges top and bottom) vs strip-rows per SIMD of that plate (232
 # useful columns per 256-column strip at depth 12, 1024 SIMDs).  Measured
 # with this build: profiles/r4_resident.md (1024 x 8192 and 2048 x 4096:
-# resident workgroup tiles), profiles/r3_tile.md (2048 x 8192, 4096 x 4096,
-# 4096 x 8192), BENCH (8192 x 8192).
+# resident workgroup tiles, r4t6), profiles/r3_tile.md (2048 x 8192,
+# 4096 x 4096: level-split pipelines), BENCH (8192 x 8192).
 RATE_POINTS: List[tuple] = [
     # (strip-rows per SIMD, Tcells/s)
-    (18.0, 2.6),    # 512 x 8192 (16-GPU-like blocks; extrapolated from the tile trend)
-    (36.0, 3.9),    # 1024 x 8192 / 2048 x 4096 (8 GPUs), resident tiles
+    (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
+    (36.0, 4.0),    # 1024 x 8192 3.99 / 2048 x 4096 4.08 (8 GPUs), resident tiles
     (72.0, 3.75),   # 2048 x 8192 / 4096 x 4096 (4 GPUs), split pipelines
     (144.0, 4.6),   # 4096 x 8192 (2 GPUs)
-    (288.0, 5.0),   # 8192 x 8192 (1 GPU)
+    (288.0, 5.1),   # 8192 x 8192 (1 GPU)
 ]
 
 SIMDS = 1024
