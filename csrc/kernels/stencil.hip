@@ -139,15 +139,19 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
 
 __global__ void judge_kernel(unsigned* resids, int n, int slots, int stride, DeviceGate* gate,
                              double eps, int mpi_compat) {
-  if (threadIdx.x != 0) return;
-  // Checks in order: the first converging one closes the gate.
+  // One wave: lane s reads (and zeroes) slot s of every check, the max over
+  // the slots is a wave reduction, lane 0 judges.  Checks in order: the
+  // first converging one closes the gate.
+  const int lane = threadIdx.x;
   for (int i = 0; i < n; ++i) {
     unsigned bits = 0u;
-    for (int s = 0; s < slots; ++s) {  // non-negative floats order like their bits
-      bits = max(bits, resids[s * stride + i]);
-      resids[s * stride + i] = 0u;
+    if (lane < slots) {
+      bits = resids[lane * stride + i];  // non-negative floats order like their bits
+      resids[lane * stride + i] = 0u;
     }
-    if (gate->stop == 0u) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) bits = max(bits, unsigned(__shfl_xor(int(bits), off)));
+    if (lane == 0 && gate->stop == 0u) {
       float r;
       __builtin_memcpy(&r, &bits, 4);
       const unsigned ordinal = gate->checks;
@@ -805,8 +809,8 @@ void checksum_block(const float* origin, int64_t pitch, int64_t lx, int64_t ly, 
 
 void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
                  int n, int slots, int stride) {
-  HEAT_CHECK(n >= 1 && slots >= 1 && (slots == 1 || stride >= n), "judge of %d checks x %d slots",
-             n, slots);
+  HEAT_CHECK(n >= 1 && slots >= 1 && slots <= 64 && (slots == 1 || stride >= n),
+             "judge of %d checks x %d slots", n, slots);
   hipLaunchKernelGGL(judge_kernel, dim3(1), dim3(64), 0, st, resid, n, slots, stride, gate, eps,
                      int(mpi_compat));
   HIP_CHECK(hipGetLastError());

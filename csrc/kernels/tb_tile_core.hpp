@@ -273,7 +273,9 @@ struct Tile {
         sink->row(r, u[r], cur);
       }
       if constexpr (ACC) {
-        if (((usemask & resmask) >> r) & 1u) acc(u[r], cur, res_lane, res_cols);
+        // Branch-free: a uniform branch per row split the step into basic
+        // blocks the scheduler cannot interleave.
+        acc_sel(u[r], cur, res_lane, res_cols, ((usemask & resmask) >> r) & 1u);
       }
       prev = cur;
       if (i == R / 2 - 1) last_nb = xc.mid();
@@ -281,6 +283,17 @@ struct Tile {
     }
   }
 
+  // acc without branches: `take` (uniform) and res_lane select the max.
+  __device__ __forceinline__ void acc_sel(const vecf& nw, const vecf& old, bool res_lane, int rc,
+                                          bool take) {
+    float d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = (j == 0 || rc > j) ? __builtin_fabsf(nw[j] - old[j]) : 0.f;
+    const float dm = __builtin_elementwise_maximum(__builtin_elementwise_maximum(d[0], d[1]),
+                                                   __builtin_elementwise_maximum(d[2], d[3]));
+    const float mm = __builtin_elementwise_maximum(m, res_lane ? dm : 0.f);
+    m = take ? mm : m;
+  }
   __device__ __forceinline__ void acc(const vecf& nw, const vecf& old, bool res_lane, int rc) {
     // NaN-propagating max (v_maximum3_f32): a NaN or inf reaches the judge.
     if (res_lane) {
