@@ -1085,7 +1085,7 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
     HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
     GraphEntry e;
     HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
-    if (tr_->world() > 1 && tr_->device_memory()) rccl_graphs_ = true;
+    if (tr_->world() > 1 && std::strcmp(tr_->name(), "rccl") == 0) rccl_graphs_ = true;
     HIP_CHECK(hipGraphDestroy(graph));
     e.cur_after = cur_;
     e.gr_after = gr_;
