@@ -137,7 +137,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // launch (increasing passes, at most one per pass, each at the pass's last
 // step: checks[c].step == depth): check c writes the max |delta| of that
 // step over the owned block [0, own_rows) x [0, own_cols) into
-// resids[slot * kTbResidentMaxChecks + c] (atomic max, tile t's slot t % 8;
+// resids[slot * kTbResidentMaxChecks + c] (atomic max per wave, 64 slots;
 // words zeroed by the caller, kTbResidentSlots * kTbResidentMaxChecks of
 // them: judge_check(resids, ..., n, kTbResidentSlots, kTbResidentMaxChecks)).
 struct TbResidentBuffers {
@@ -266,8 +266,9 @@ struct DeviceGate {
 void judge_check(unsigned* resid, DeviceGate* gate, double eps, bool mpi_compat, hipStream_t st,
                  int n = 1, int slots = 1, int stride = 0);
 // The resident span's residual block: kTbResidentSlots lines of
-// kTbResidentMaxChecks words (TbResidentBuffers / tb_resident_step resids).
-constexpr int kTbResidentSlots = 8;
+// kTbResidentMaxChecks words (TbResidentBuffers / tb_resident_step resids);
+// wave w of tile t adds to slot (t * waves + w) % kTbResidentSlots.
+constexpr int kTbResidentSlots = 64;
 
 // Max |a-b| over a box (standalone residual), atomically into *resid.
 void residual_box(const float* a, const float* b, int64_t pitch, const Box& box, unsigned* resid,

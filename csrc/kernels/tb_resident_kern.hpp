@@ -42,31 +42,24 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // Neighbour waits give up after this many polls (~0.3 s with s_sleep 2).
 constexpr unsigned kSpinLimit = 1u << 22;
 
-// One max per workgroup into *word (a non-negative float's bits order like
-// the float; NaN has its sign cleared by fabs).  Every thread calls it.
-template <int NW>
-__device__ __forceinline__ void wg_max_atomic(float m, unsigned* word, unsigned* wmax) {
+// One max per WAVE into *word (a non-negative float's bits order like the
+// float; NaN has its sign cleared by fabs): no workgroup barrier in the
+// pass (two per check cost ~1.5 us per check pass); the callers spread the
+// waves over kTbResidentSlots words, so an address takes ~130 atomics.
+__device__ __forceinline__ void wave_max_atomic_u(float m, unsigned* word) {
   unsigned mm = __float_as_uint(m);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) mm = max(mm, unsigned(__shfl_xor(int(mm), off)));
-  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mm;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned r = 0u;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) r = max(r, wmax[i]);
-    atomicMax(word, r);
-  }
-  __syncthreads();  // wmax is reused by the next check
+  if ((threadIdx.x & 63) == 0) atomicMax(word, mm);
 }
 
 // RES 1: the residuals of the checks inside the launch (ResArgs::chk_*),
-// each at the last step of its pass (tile_pass_steps ACC_MODE 2); the
-// workgroup's max goes to the check's word at the end of that pass.  A
+// each at the last step of its pass (tile_pass_steps ACC_MODE 2); each
+// wave's max goes to the check's word of its slot at the end of that pass.  A
 // separate instantiation: the RES 0 kernel keeps its register allocation.
 template <int R, int NW, int MODE, int XL, int RES>
 __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
-                                             int u, vecf (*xch)[2][NW][64], unsigned* wmax) {
+                                             int u, vecf (*xch)[2][NW][64]) {
   const TbArgs& a = ra.a;
   const int K = ra.depth;
   const int lane = threadIdx.x & 63;
@@ -196,7 +189,8 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     });
     if constexpr (RES == 1) {
       if (ci >= 0) {
-        wg_max_atomic<NW>(T.m, ra.resids + (u & (kTbResidentSlots - 1)) * kResMaxChecks + ci, wmax);
+        const int slot = (u * NW + w) & (kTbResidentSlots - 1);
+        wave_max_atomic_u(T.m, ra.resids + slot * kResMaxChecks + ci);
         T.m = 0.f;
       }
     }
@@ -280,9 +274,8 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t wx_lo = g.gx0 + ub - K + int64_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * R;
   const int64_t wx_hi = wx_lo + R - 1;
   const int mode = (ra.diag & 8) ? kTileGeneric : tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi);
-  __shared__ unsigned wmax[NW];
   tile_dispatch<XL>(mode, [&](auto mode_c) {
-    resident_run<R, NW, decltype(mode_c)::value, XL, RES>(ra, bx, strip, t, blk, xch, wmax);
+    resident_run<R, NW, decltype(mode_c)::value, XL, RES>(ra, bx, strip, t, blk, xch);
     return 0.f;
   });
   // Completion: the tile that finishes last (every other tile is past its
