@@ -139,31 +139,38 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
 
 __global__ void judge_kernel(unsigned* resids, int n, int slots, int stride, DeviceGate* gate,
                              double eps, int mpi_compat) {
-  // One wave: lane s reads (and zeroes) slot s of every check, the max over
-  // the slots is a wave reduction, lane 0 judges.  Checks in order: the
-  // first converging one closes the gate.
+  // One wave: lane s reads (and zeroes) slot s of every check -- all loads
+  // issued before the first use --, the max over the slots is a wave
+  // reduction, lane 0 judges.  Checks in order: the first converging one
+  // closes the gate.
+  constexpr int kMax = 32;  // kTbResidentMaxChecks; longer lists loop
   const int lane = threadIdx.x;
-  for (int i = 0; i < n; ++i) {
-    unsigned bits = 0u;
-    if (lane < slots) {
-      bits = resids[lane * stride + i];  // non-negative floats order like their bits
-      resids[lane * stride + i] = 0u;
-    }
+  for (int i0 = 0; i0 < n; i0 += kMax) {
+    const int m = min(n - i0, kMax);
+    unsigned v[kMax];
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) bits = max(bits, unsigned(__shfl_xor(int(bits), off)));
-    if (lane == 0 && gate->stop == 0u) {
-      float r;
-      __builtin_memcpy(&r, &bits, 4);
-      const unsigned ordinal = gate->checks;
-      gate->checks = ordinal + 1u;
-      gate->last_bits = bits;
-      unsigned why = 0u;
-      if ((bits & 0x7F800000u) == 0x7F800000u) why = 2u;  // inf or NaN
-      else if (mpi_compat ? double(r) <= eps : r < float(eps)) why = 1u;
-      if (why) {
-        gate->reason = why;
-        gate->stop_check = ordinal;
-        gate->stop = 1u;
+    for (int j = 0; j < kMax; ++j) v[j] = (j < m && lane < slots) ? resids[lane * stride + i0 + j] : 0u;
+#pragma unroll
+    for (int j = 0; j < kMax; ++j)
+      if (j < m && lane < slots) resids[lane * stride + i0 + j] = 0u;
+    for (int j = 0; j < m; ++j) {
+      unsigned bits = v[j];  // non-negative floats order like their bits
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) bits = max(bits, unsigned(__shfl_xor(int(bits), off)));
+      if (lane == 0 && gate->stop == 0u) {
+        float r;
+        __builtin_memcpy(&r, &bits, 4);
+        const unsigned ordinal = gate->checks;
+        gate->checks = ordinal + 1u;
+        gate->last_bits = bits;
+        unsigned why = 0u;
+        if ((bits & 0x7F800000u) == 0x7F800000u) why = 2u;  // inf or NaN
+        else if (mpi_compat ? double(r) <= eps : r < float(eps)) why = 1u;
+        if (why) {
+          gate->reason = why;
+          gate->stop_check = ordinal;
+          gate->stop = 1u;
+        }
       }
     }
   }
