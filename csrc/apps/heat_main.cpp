@@ -308,7 +308,8 @@ int main(int argc, char** argv) {
     // Memory plan without allocating: the two fields of
     // every rank's block plus its ghost ring at the deepest halo the solver
     // picks (depth 12 x 8 passes per exchange = 96, or --tb-depth x
-    // --halo-passes), E/W and corner halo buffers; the worst rank decides.
+    // --halo-passes), E/W and corner halo buffers, the resident tiles'
+    // exchange fields on small blocks; the worst rank decides.
     const int ranks = std::max(gpus, env_i("WORLD_SIZE", 1));
     const Cart cart(ranks, P.decomp, P.px, P.py, P.nx, P.ny);
     const int depth = P.tb_depth > 0 ? P.tb_depth : 12;
@@ -321,6 +322,10 @@ int main(int argc, char** argv) {
       if (cart.py > 1) h = std::min<int64_t>(h, b.ly);
       const Layout L = Layout::make(b.lx, b.ly, int(std::max<int64_t>(1, h)));
       int64_t bytes = 2 * L.bytes();
+      // Resident workgroup tiles (blocks under 64 strip-rows per SIMD on the
+      // 1024 SIMDs of an MI355X) add two exchange fields of the same layout.
+      const int64_t strip = 256 - 2 * ((depth + 3) / 4 * 4);
+      if ((b.ly + strip - 1) / strip * b.lx < 64 * 1024) bytes += 2 * L.bytes();
       if (cart.py > 1) bytes += 4 * b.lx * h * 4;
       if (cart.px > 1 && cart.py > 1) bytes += 8 * h * h * 4;
       if (bytes > worst) worst = bytes, worst_rank = r;
