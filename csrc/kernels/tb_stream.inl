@@ -1035,19 +1035,10 @@ bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
       if (args.flags & tbdetail::kTbLinear) launch_split_k<8, 4, 0, 1>(args, st);
       else launch_split_k<8, 4, 0, 0>(args, st);
       return true;
-    case 12: {
-      // HEAT_TB_SPLIT_K1 (experiment): levels of stage 0 (the loading wave)
-      // on classic plans, 5 / 6 / 7.
-      static const int k1 = [] {
-        const char* e = std::getenv("HEAT_TB_SPLIT_K1");
-        return e && *e ? std::atoi(e) : 6;
-      }();
+    case 12:
       if (args.flags & tbdetail::kTbLinear) launch_split_k<12, 6, 0, 1>(args, st);
-      else if (k1 == 5) launch_split_k<12, 5, 0, 0>(args, st);
-      else if (k1 == 7) launch_split_k<12, 7, 0, 0>(args, st);
       else launch_split_k<12, 6, 0, 0>(args, st);
       return true;
-    }
     default: return false;
   }
 }
@@ -1055,13 +1046,7 @@ bool launch_split(const TbArgs& args, int depth, hipStream_t st) {
 int occupancy_split(int depth) {
   switch (depth) {
     case 8: return occ_split_k<8, 4>();
-    case 12: {
-      static const int k1 = [] {
-        const char* e = std::getenv("HEAT_TB_SPLIT_K1");
-        return e && *e ? std::atoi(e) : 6;
-      }();
-      return k1 == 5 ? occ_split_k<12, 5>() : k1 == 7 ? occ_split_k<12, 7>() : occ_split_k<12, 6>();
-    }
+    case 12: return occ_split_k<12, 6>();
     default: return 1;
   }
 }
