@@ -44,8 +44,20 @@ configuration (Heat.pdf p.8-11 Paraver phases, as numbers).
 Failure handling: RCCL must come up on every rank (the ranks agree through
 torch.distributed before going on); if it fails anywhere the run exits
 non-zero, unless `--allow-fallback` lets ALL ranks switch together to halos
-staged through host memory (named in config.parallelism).  A watchdog ends a
-hung run with a stack dump instead of letting it hang (`--watchdog-s`).
+staged through host memory (named in config.parallelism).  A resident-tile
+launch that gives up a neighbour wait (tiles not co-resident) invalidates its
+run: the ranks agree on that after the warmup and after the timed steps
+(outside the timed region), rebuild the solver with one launch per pass and
+measure again.  The autotune skips a candidate that fails cleanly at run time
+(every rank at the same point, communicator intact) instead of aborting.
+Every such step is listed in "fallbacks" (empty when none was taken).  A
+watchdog ends a hung run with a stack dump instead of letting it hang
+(`--watchdog-s`).
+
+Exchange model (multi-GPU): before pruning autotune candidates, grouped halo
+exchanges of the first candidate are timed at two depths on the real ranks;
+the fitted latency and per-link GB/s replace the stated constants of
+parallel/model.py in the pruning and in "predicted" / "model".
 """
 from __future__ import annotations
 
@@ -158,6 +170,11 @@ def main() -> int:
             faulthandler.dump_traceback_later(seconds, exit=True)
 
     watchdog("init", args.watchdog_s)
+    # A resident-tile give-up (tiles not co-resident) is reported by the run
+    # instead of raised: the ranks agree on it and redo the work without
+    # resident spans ("fallbacks" in the JSON line).
+    os.environ.setdefault("HEAT_TB_RES_GIVEUP", "defer")
+    fallbacks = []
     device = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(device)
     rccl_log = None
@@ -221,23 +238,33 @@ def main() -> int:
                 return 1
             log(rank, "falling back to host-staged halos over gloo (all ranks)")
             shared = EngineTransport("torch", info, group=dist.new_group(backend="gloo"))
+            fallbacks.append({"what": f"RCCL transport failed on some rank ({err})",
+                              "action": "host-staged halos over gloo (--allow-fallback)"})
 
     tuning = None
     pruned = []
+    xgmi = None
     if world > 1 and not args.no_autotune:
         # The fastest decomposition (rows slabs vs the 2-D dims_create grid)
         # and pass schedule depend on xGMI link bandwidth and the per-rank
         # block shape: time each on the real ranks before the timed region.
-        from parallel_heat_amd.parallel.model import predict, prune
-        from parallel_heat_amd.parallel.tune import autotune, default_candidates, describe
+        from parallel_heat_amd.parallel.model import fit_exchange, predict, prune
+        from parallel_heat_amd.parallel.tune import (autotune, default_candidates, describe,
+                                                     measure_exchange)
 
         watchdog("autotune", args.watchdog_s)
         all_cands = default_candidates(cfg, world,
                                        schedules=[x for x in args.autotune_schedules.split(",") if x],
                                        halo_passes=[int(x) for x in
                                                     args.autotune_halo_passes.split(",") if x])
-        cands = prune(all_cands, world)
-        pruned = [dict(describe(c, world), predicted_ms_per_1000=predict(c, world)["ms_per_1000"])
+        # The exchange model's latency and bandwidth, measured on these ranks
+        # (grouped exchanges of the first candidate's messages at two depths)
+        # before they prune anything.
+        xgmi = exchange_probe(all_cands[0], info, shared, world, HeatSolver, measure_exchange,
+                              fit_exchange, rank)
+        cands = prune(all_cands, world, xgmi=xgmi)
+        pruned = [dict(describe(c, world),
+                       predicted_ms_per_1000=predict(c, world, xgmi=xgmi)["ms_per_1000"])
                   for c in all_cands if c not in cands]
         try:
             cfg, tuning = autotune(cfg, info, cands, steps=args.iters_per_step, repeats=3,
@@ -246,6 +273,8 @@ def main() -> int:
         except _native.NativeError as e:
             # Every candidate rejected (the ranks agree inside autotune).
             log(rank, f"autotune failed ({e}); using --decomp {args.decomp}")
+            fallbacks.append({"what": f"autotune failed ({str(e)[:160]})",
+                              "action": f"--decomp {args.decomp} as given"})
 
     solver = None
     err = None
@@ -263,26 +292,54 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
-    watchdog("warmup", args.watchdog_s)
-    for _ in range(args.warmup):
-        solver.run(args.iters_per_step)
-    barrier()
-    torch.cuda.synchronize()
-    watchdog("timed", args.watchdog_s)
-    t0 = time.perf_counter()
-    done = 0
-    phases = [0.0, 0.0, 0.0]
-    for _ in range(args.steps):
-        r = solver.run(args.iters_per_step)
-        done += r.steps_done
-        phases = [phases[0] + r.t_exchange, phases[1] + r.t_compute, phases[2] + r.t_reduce]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    def measure():
+        """Warmup, then the timed region.  None if a resident launch gave up
+        on any rank (the ranks agree outside the timed region)."""
+        watchdog("warmup", args.watchdog_s)
+        gave = 0
+        for _ in range(args.warmup):
+            gave += solver.run(args.iters_per_step).resident_giveups
+        if not vote(gave == 0):
+            return None
+        barrier()
+        torch.cuda.synchronize()
+        watchdog("timed", args.watchdog_s)
+        t0 = time.perf_counter()
+        done = 0
+        phases = [0.0, 0.0, 0.0]
+        for _ in range(args.steps):
+            r = solver.run(args.iters_per_step)
+            done += r.steps_done
+            gave += r.resident_giveups
+            phases = [phases[0] + r.t_exchange, phases[1] + r.t_compute, phases[2] + r.t_reduce]
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if not vote(gave == 0):
+            return None
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), done, phases
+
+    res = measure()
+    if res is None:
+        # Resident tiles were not co-resident somewhere (another process on a
+        # GPU, ...): the state is invalid.  Every rank rebuilds its solver
+        # with one launch per pass and measures again from the initial state.
+        log(rank, "a resident launch gave up on some rank: measuring again without resident spans")
+        fallbacks.append({"what": "resident tiles gave up a neighbour wait on some rank "
+                                  "(state invalid)",
+                          "action": "solver rebuilt with HEAT_TB_RESIDENT=0 (one launch per "
+                                    "pass), warmup and timed steps run again"})
+        solver.close()
+        os.environ["HEAT_TB_RESIDENT"] = "0"
+        solver = HeatSolver(cfg, dist_info=info, shared=shared)
+        res = measure()
+        if res is None:
+            log(rank, "resident give-up with resident spans off: giving up")
+            return 1
+    elapsed, done, phases = res
 
     verified = None
     check = {}
@@ -294,7 +351,7 @@ def main() -> int:
         # Untimed: the model's prediction for the chosen layout and the
         # measured per-rank phase split of one eager phase-timed run.
         watchdog("explain", args.watchdog_s)
-        explain = explain_run(cfg, info, shared, world, args.iters_per_step, HeatSolver)
+        explain = explain_run(cfg, info, shared, world, args.iters_per_step, HeatSolver, xgmi)
     rccl = None
     if shared is not None:
         # What the engine's communicator saw, from every rank: its rank count
@@ -344,6 +401,7 @@ def main() -> int:
                                    if args.converge else False),
             },
             "verified": verified,
+            "fallbacks": fallbacks,
         }
         if tuning is not None:
             line["autotune"] = tuning
@@ -370,7 +428,28 @@ def main() -> int:
     return 0 if verified is not False else 2
 
 
-def explain_run(cfg, info, shared, world, iters, HeatSolver):
+def exchange_probe(cfg, info, shared, world, HeatSolver, measure_exchange, fit_exchange, rank):
+    """Measured exchange parameters (latency, GB/s per link) from grouped halo
+    exchanges of cfg's layout at its full halo depth and a quarter of it, max
+    over the ranks (collective); None (the stated model) if the probe fails
+    on any rank."""
+    pts = None
+    try:
+        with HeatSolver(cfg, dist_info=info, shared=shared) as s:
+            H = s.info.halo
+            def agree_max(x):
+                t = torch.tensor([x], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                return float(t.item())
+            pts = measure_exchange(s, sorted({H, max(1, H // 4)}), iters=10, agree_max=agree_max)
+    except Exception as e:  # noqa: BLE001 - diagnostics; the stated model stays
+        log(rank, f"exchange probe failed ({e})")
+    ok = torch.tensor([1 if pts else 0], dtype=torch.int32, device="cuda")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return fit_exchange(pts) if ok.item() else None
+
+
+def explain_run(cfg, info, shared, world, iters, HeatSolver, xgmi=None):
     """Model prediction + measured per-rank phase split (collective)."""
     from parallel_heat_amd.parallel.model import model_params, predict
     phases = {"exchange": None, "compute": None, "reduce": None}
@@ -387,7 +466,7 @@ def explain_run(cfg, info, shared, world, iters, HeatSolver):
         phases["error"] = str(e)[:200]
     every = [None] * world
     dist.all_gather_object(every, dict(phases, rank=info.rank))
-    return {"predicted": predict(cfg, world), "model": model_params(),
+    return {"predicted": predict(cfg, world, xgmi=xgmi), "model": model_params(xgmi),
             "phase_seconds_per_1000": every}
 
 

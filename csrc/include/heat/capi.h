@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define HEAT_ABI_VERSION 4
+#define HEAT_ABI_VERSION 5
 
 typedef struct heat_params {
   int64_t nx, ny;
@@ -65,6 +65,7 @@ typedef struct heat_run_stats {
   int64_t passes, exchanges, checks;
   double t_exchange, t_compute, t_reduce; /* seconds per phase (phase_timing) */
   int64_t resident_passes;                /* passes run inside resident-tile launches */
+  int64_t resident_giveups;               /* 1: a resident launch gave up (HEAT_TB_RES_GIVEUP=defer) */
 } heat_run_stats;
 
 typedef struct heat_block_info {
@@ -127,6 +128,10 @@ int heat_group_transport(const char* requested, int world, const int32_t* device
 /* Give up this rank: abort its transport (ncclCommAbort) so peers stop
    waiting; a wait of the solver on another thread throws.  Thread-safe. */
 int heat_solver_abort(heat_solver* s);
+/* Seconds per grouped halo exchange of `depth` rows/columns on this rank
+   (device time over `iters` exchanges) and its largest message; collective. */
+int heat_solver_time_exchange(heat_solver* s, int depth, int iters, double* seconds,
+                              int64_t* max_bytes);
 /* 1 if the automatic TB variant at `depth` takes a residual at any inner step
    (checks ride inside full-depth passes), else 0. */
 int heat_tb_mid_residual(int depth);

@@ -57,6 +57,9 @@ struct RunStats {
   // summed over launches, so concurrent phases may add up to > seconds).
   double t_exchange = 0.0, t_compute = 0.0, t_reduce = 0.0;
   int64_t resident_passes = 0;  // passes run inside resident-tile launches
+  // 1: a resident launch of this call gave up a neighbour wait (results
+  // invalid; only returned with HEAT_TB_RES_GIVEUP=defer, else run throws).
+  int64_t resident_giveups = 0;
 };
 
 class Solver {
@@ -74,6 +77,10 @@ class Solver {
   // queued collectives would otherwise wait for peers forever (and the
   // destructor's device syncs with them).
   RunStats run(int64_t steps);
+  // Seconds per grouped halo exchange of `depth` rows/columns (device time
+  // over `iters` back-to-back exchanges, this rank); *max_bytes: the largest
+  // message.  Collective.  Feeds the autotune's exchange model.
+  double time_exchange(int depth, int iters, int64_t* max_bytes);
   // Run the configured number of steps (Params::steps given at construction
   // by the caller; compat=mpi adds one).
   int64_t configured_steps(int64_t steps) const;
@@ -215,6 +222,8 @@ class Solver {
   bool resident_ = false;  // resident-tile launches enabled for this solver
   bool resident_force_ = false;  // HEAT_TB_RESIDENT=2: also with ranks sharing the device
   bool resident_used_ = false;  // one was enqueued in this run (check its error word)
+  bool defer_giveup_ = false;   // HEAT_TB_RES_GIVEUP=defer: report a give-up, do not throw
+  bool inject_giveup_ = false;  // HEAT_TEST_RES_GIVEUP_RANK: fake one give-up (tests)
   float* xbase_[2] = {nullptr, nullptr};  // their exchange fields
   unsigned* d_flags_ = nullptr;           // + per-tile flags and the error word
   unsigned* h_err_ = nullptr;             // pinned copy of the error word

@@ -499,6 +499,12 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     for (int b = 0; b < nbox; ++b)
       if (!boxes[b].empty()) rows4 += ceil_div(boxes[b].cols(), W4) * boxes[b].rows();
     variant = tb_auto_variant(depth, rows4 / tb_simd_count());
+    // Even depths only the tile kernel builds (10, 14, 16: checks every 10k
+    // steps on tile-sized blocks) stay on it whatever the launch size: a
+    // deep-halo box grown past the tile threshold (Solver::tile_sized_at
+    // judges the owned block) is still a valid tile launch, only slower.
+    if (!tb_depth_supported(depth) && depth % 2 == 0 && depth <= 16)
+      variant = tbv::kTile | tbv::kXcdGroups;
   }
   // The tile kernel takes any even depth up to 16 (Solver picks 10 for
   // checks every 10k steps on tile-sized blocks); the streaming kernels the

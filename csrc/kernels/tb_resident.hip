@@ -30,7 +30,10 @@
 // Double-buffered exchange fields make the protocol race-free: a tile
 // rewrites xb[p & 1] at the end of pass p + 2 only after it has seen every
 // neighbour's flag p + 2, i.e. after every neighbour finished the pass p + 1
-// that read it.  Flags are zeroed by a memset node before every launch
+// that read it.  Flags and the completion counter are zero at every launch:
+// zeroed once when the buffers are allocated, then re-zeroed by the tile that
+// finishes last (the completion counter tells it; every other tile is past
+// its last poll by then), in place of a memset node per launch
 // (cdna_hip_programming.md Guideline 16, "Re-initialise every call"); every
 // spin is bounded and reports through *err instead of hanging the device.
 //

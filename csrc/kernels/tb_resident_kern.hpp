@@ -297,20 +297,25 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   }
 }
 
-template <int R, int NW, int XL>
-int occ_res() {
+template <class Kern>
+int occ_kernel(Kern k, int NW) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tile_resident_kernel<R, NW, XL, 0>, 64 * NW, 0) !=
-      hipSuccess)
-    n = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * NW, 0) != hipSuccess) n = 1;
   hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tile_resident_kernel<R, NW, XL, 0>)) ==
-          hipSuccess &&
-      fa.numRegs > 0) {
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k)) == hipSuccess && fa.numRegs > 0) {
     const int alloc = (fa.numRegs + 7) / 8 * 8;
     n = std::min(n, (512 / alloc) / (NW / 4));
   }
   return std::max(0, n);
+}
+
+// Co-resident tiles per CU: the smaller of the two instantiations (the RES 1
+// build takes more VGPRs, e.g. 128 vs 106 at 12 x 8), so a plan accepted for
+// an unchecked span stays co-resident when its span carries checks.
+template <int R, int NW, int XL>
+int occ_res() {
+  return std::min(occ_kernel(tile_resident_kernel<R, NW, XL, 0>, NW),
+                  occ_kernel(tile_resident_kernel<R, NW, XL, 1>, NW));
 }
 
 // Instantiated shapes (rows per wave, waves per workgroup): the tile

@@ -282,7 +282,18 @@ int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out) {
       out->exchanges = r.exchanges;
       out->checks = r.checks;
       out->resident_passes = r.resident_passes;
+      out->resident_giveups = r.resident_giveups;
     }
+  });
+}
+
+int heat_solver_time_exchange(heat_solver* s, int depth, int iters, double* seconds,
+                              int64_t* max_bytes) {
+  return guard([&] {
+    int64_t b = 0;
+    const double t = s->s->time_exchange(depth, iters, &b);
+    if (seconds) *seconds = t;
+    if (max_bytes) *max_bytes = b;
   });
 }
 

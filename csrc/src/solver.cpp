@@ -124,13 +124,21 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   // sight (device count >= world) and no other solver of this process on
   // the device (resident_span).  HEAT_TB_RESIDENT=2 skips that check (tests
   // whose ranks' grids all fit the one GPU together), 0 disables.
+  // The ranks that can share this node's GPUs are the local ones
+  // (LOCAL_WORLD_SIZE under torchrun; the whole world otherwise), so a
+  // multi-node run with a GPU per local rank still goes resident.
   int ndev = 0;
   if (on_gpu() && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  const int local_world = std::min(world, std::max(1, env_int("LOCAL_WORLD_SIZE", world)));
   const int res_env = env_int("HEAT_TB_RESIDENT", 1);
   resident_force_ = res_env == 2;
   resident_ = tile_sized() && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
               !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
-              (world == 1 || ndev >= world || resident_force_);
+              (world == 1 || ndev >= local_world || resident_force_);
+  if (const char* e = std::getenv("HEAT_TB_RES_GIVEUP"); e && std::strcmp(e, "defer") == 0)
+    defer_giveup_ = true;
+  // Tests: this rank's first run with resident spans reports a give-up.
+  inject_giveup_ = resident_ && env_int("HEAT_TEST_RES_GIVEUP_RANK", -1) == tr_->rank();
   host_checks_ = env_int("HEAT_HOST_CHECKS", 0) != 0;
   timing_ = P_.phase_timing || env_int("HEAT_PHASE_TIMING", 0) != 0;
   // Waits on the device poll the transport and give up after this long
@@ -1252,8 +1260,18 @@ void Solver::replay_check(const PassRec& p) {
     compute_gpu(p.k, 0, false, 0, 0, p.er, p.ec);
     cur_ ^= 1;
   }
-  compute_gpu(p.rl, 0, false, 0, 0, p.span > 1 ? p.er : 0, p.span > 1 ? p.ec : 0);
-  cur_ ^= 1;
+  // The check's rl steps as passes tb_step takes (a check at level 9-11 of a
+  // depth-12 pass is no depth of its own): rl mod 8 first, then 8-step passes.
+  // Each sub-pass covers the box grown by the steps still to come (a multiple
+  // of 4, so the column growth is exact and float4-aligned); that needs at
+  // most rl <= k valid ghost levels, which the pass itself had.
+  const int64_t er0 = p.span > 1 ? p.er : 0, ec0 = p.span > 1 ? p.ec : 0;
+  for (int left = p.rl; left > 0;) {
+    const int d = gpu::tb_depth_supported(left) ? left : (left % 8 != 0 ? left % 8 : 8);
+    left -= d;
+    compute_gpu(d, 0, false, 0, 0, std::max<int64_t>(er0, left), std::max<int64_t>(ec0, left));
+    cur_ ^= 1;
+  }
   gr_ = gc_ = 0;  // the replayed buffer's ghosts are stale
   sync_watch();
 }
@@ -1261,9 +1279,8 @@ void Solver::replay_check(const PassRec& p) {
 RunStats Solver::run(int64_t steps) {
   try {
     return run_impl(steps);
-  } catch (...) {
+  } catch (const std::exception& e) {
     if (tr_->world() > 1) {
-      std::fprintf(stderr, "[heat] rank %d: run failed; aborting\n", tr_->rank());
       if (capturing_) {
         // Drop the half-built capture (its stream is unusable otherwise).
         hipGraph_t g = nullptr;
@@ -1271,12 +1288,62 @@ RunStats Solver::run(int64_t steps) {
         if (g) (void)hipGraphDestroy(g);
         capturing_ = false;
       }
+      // A failure after which this rank's queued work still completes (every
+      // exchange and all-reduce it enqueued was matched, no transport error):
+      // a planning check or a non-finite residual, which every rank meets at
+      // the same point since those decisions are global.  The communicator
+      // stays usable; the message says so ("[clean]"), so a caller that
+      // agrees with its peers (parallel.tune.autotune) can go on.  Anything
+      // else aborts it so that peers waiting on this rank fail instead of
+      // hanging.
+      bool clean = false;
+      if (on_gpu() && !aborted_.load() && !staged_failed_.load()) {
+        try {
+          sync_watch();
+          tr_->check();
+          clean = true;
+        } catch (...) {
+        }
+      }
+      if (clean) {
+        std::fprintf(stderr, "[heat] rank %d: run failed after its queued work completed; "
+                             "communicator kept\n", tr_->rank());
+        throw Error(std::string("[clean] ") + e.what());
+      }
+      std::fprintf(stderr, "[heat] rank %d: run failed; aborting\n", tr_->rank());
       abort();
       std::fprintf(stderr, "[heat] rank %d: aborted%s\n", tr_->rank(),
                    rccl_graphs_.load() ? " (communicator left to process exit: live graphs)" : "");
     }
     throw;
   }
+}
+
+double Solver::time_exchange(int depth, int iters, int64_t* max_bytes) {
+  // One grouped exchange phase of `depth` rows / columns (the message list a
+  // run's deep-halo exchange sends), timed on the device over `iters`
+  // back-to-back phases after one untimed phase (RCCL connections).  A halo
+  // exchange of the current buffer is idempotent.  Collective: every rank
+  // calls it with the same arguments.  Returns seconds per exchange.
+  HEAT_CHECK(on_gpu() && tr_->world() > 1, "time_exchange needs GPU ranks");
+  HEAT_CHECK(depth >= 1 && depth <= H_ && iters >= 1, "time_exchange depth %d (halo %d)", depth, H_);
+  if (max_bytes) {
+    const int64_t ns = (cart_.px > 1) ? int64_t(depth) * L_.pitch * 4 : 0;
+    const int64_t ew = (cart_.py > 1) ? blk_.lx * int64_t(depth) * 4 : 0;
+    *max_bytes = std::max(ns, ew);
+  }
+  synchronize();
+  exchange(cur_, depth, s_comp_);
+  sync_watch();
+  hipEvent_t a = pooled_event(), b = pooled_event();
+  HIP_CHECK(hipEventRecord(a, s_comp_));
+  for (int i = 0; i < iters; ++i) exchange(cur_, depth, s_comp_);
+  HIP_CHECK(hipEventRecord(b, s_comp_));
+  sync_watch();
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+  pool_used_ = 0;
+  return 1e-3 * double(ms) / iters;
 }
 
 RunStats Solver::run_impl(int64_t steps) {
@@ -1306,14 +1373,41 @@ RunStats Solver::run_impl(int64_t steps) {
     if (gated()) run_gated(steps, s);
     else run_segments(steps, s);
   }
-  if (resident_used_)
-    HIP_CHECK(hipMemcpyAsync(h_err_, d_flags_ + kResidentFlagBytes / 4, 4, hipMemcpyDeviceToHost,
-                             s_comp_));
+  unsigned* d_err = resident_used_ ? d_flags_ + kResidentFlagBytes / 4 : nullptr;
+  if (d_err) HIP_CHECK(hipMemcpyAsync(h_err_, d_err, 4, hipMemcpyDeviceToHost, s_comp_));
   sync_watch();
-  if (resident_used_ && *h_err_ != 0)
-    throw_error(__FILE__, __LINE__,
-                "resident tile launch: a neighbour wait gave up (tiles not co-resident?); "
-                "results are invalid (HEAT_TB_RESIDENT=0 runs one launch per pass)");
+  bool gave_up = d_err && *h_err_ != 0;
+  if (gave_up) {
+    // Clear it for the next launch (the flags and the completion counter
+    // were re-zeroed by the last tile, which every tile reaches).
+    *h_err_ = 0;
+    HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+  }
+  if (d_err && inject_giveup_) {  // HEAT_TEST_RES_GIVEUP_RANK (tests)
+    inject_giveup_ = false;
+    gave_up = true;
+  }
+  if (gave_up) {
+    // A neighbour wait gave up (tiles not co-resident, e.g. another process
+    // holds CUs): this run's results are invalid.  All of its exchanges and
+    // collectives were matched (the spans make the same transport calls as
+    // separate passes), so nothing is left waiting.  Default: throw.  With
+    // HEAT_TB_RES_GIVEUP=defer (bench.py, the autotune) the run returns with
+    // resident_giveups set and resident spans switched off for this solver,
+    // and the caller -- which agrees with its peers -- redoes the work.
+    if (!defer_giveup_)
+      throw_error(__FILE__, __LINE__,
+                  "resident tile launch: a neighbour wait gave up (tiles not co-resident?); "
+                  "results are invalid (HEAT_TB_RESIDENT=0 runs one launch per pass)");
+    std::fprintf(stderr, "[heat] rank %d: resident tiles gave up a neighbour wait: this run's "
+                         "results are invalid; resident spans off for this solver\n", tr_->rank());
+    resident_ = false;
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second.exec);
+    graphs_.clear();
+    rccl_graphs_ = false;
+    s.resident_giveups = 1;
+  }
   check_staged();
   tr_->check();
   s.seconds = now_s() - t0;

@@ -43,7 +43,7 @@ class RcclTransport final : public Transport {
     if (abandoned_) return;
     if (scratch_) (void)hipFree(scratch_);
     std::lock_guard<std::mutex> lk(mu_);
-    if (comm_) (void)ncclCommDestroy(comm_);
+    if (comm_ && !aborted_.load()) (void)ncclCommDestroy(comm_);
   }
   void abandon() override { abandoned_ = true; }
   int rank() const override { return rank_; }
@@ -103,11 +103,14 @@ class RcclTransport final : public Transport {
                   std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
   }
   // ncclCommAbort: RCCL's kernels and proxy threads stop waiting for peers
-  // that will never answer; later calls throw.  Idempotent.
+  // that will never answer; later calls throw.  Idempotent.  Not under mu_:
+  // a peer thread of a single-process group can hold it while blocked in
+  // ncclGroupEnd waiting for the dead rank, and the abort is what unblocks
+  // it (ncclCommAbort is meant to be called from another thread).  comm_
+  // keeps its value; the flag turns every later call away (live()).
   void abort() override {
-    std::lock_guard<std::mutex> lk(mu_);
+    if (aborted_.exchange(true)) return;
     if (comm_) (void)ncclCommAbort(comm_);
-    comm_ = nullptr;
   }
   const char* name() const override { return "rccl"; }
   TransportInfo info() const override {
@@ -124,11 +127,11 @@ class RcclTransport final : public Transport {
 
  private:
   void live() const {
-    if (!comm_) throw_error(__FILE__, __LINE__, "RCCL communicator was aborted");
+    if (!comm_ || aborted_.load()) throw_error(__FILE__, __LINE__, "RCCL communicator was aborted");
   }
   int rank_, world_;
   mutable std::mutex mu_;
-  std::atomic<bool> abandoned_{false};
+  std::atomic<bool> abandoned_{false}, aborted_{false};
   ncclComm_t comm_ = nullptr;
   float* scratch_ = nullptr;
 };

@@ -22,7 +22,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be imported before libheat: shared HIP runtime)
 
-ABI_VERSION = 4  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
+ABI_VERSION = 5  # must match HEAT_ABI_VERSION in csrc/include/heat/capi.h
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
@@ -82,7 +82,7 @@ class HeatRunStats(Structure):
         ("last_resid", c_float), ("seconds", c_double),
         ("passes", c_int64), ("exchanges", c_int64), ("checks", c_int64),
         ("t_exchange", c_double), ("t_compute", c_double), ("t_reduce", c_double),
-        ("resident_passes", c_int64),
+        ("resident_passes", c_int64), ("resident_giveups", c_int64),
     ]
 
 
@@ -183,6 +183,8 @@ _SIGS = {
     "heat_tb_mid_residual": (c_int, [c_int]),
     "heat_group_transport": (c_int, [ctypes.c_char_p, c_int, POINTER(c_int32), POINTER(c_int32)]),
     "heat_solver_abort": (c_int, [c_void_p]),
+    "heat_solver_time_exchange": (c_int, [c_void_p, c_int, c_int, POINTER(c_double),
+                                          POINTER(c_int64)]),
 }
 
 

@@ -40,6 +40,9 @@ class RunResult:
     t_compute: float = 0.0   # seconds in stencil kernels
     t_reduce: float = 0.0    # seconds in residual all-reduce + read-back
     resident_passes: int = 0  # passes run inside resident-tile launches (tiles kept in VGPRs)
+    # 1: a resident launch gave up a neighbour wait (results invalid); only
+    # returned with HEAT_TB_RES_GIVEUP=defer, otherwise run() raises.
+    resident_giveups: int = 0
 
     @property
     def mcells_per_s(self) -> float:
@@ -186,7 +189,16 @@ class HeatSolver:
         return RunResult(st.steps_done, st.total_steps, bool(st.converged), st.converged_at,
                          st.last_resid, st.seconds, st.passes, st.exchanges, st.checks,
                          self.config.nx * self.config.ny, st.t_exchange, st.t_compute,
-                         st.t_reduce, st.resident_passes)
+                         st.t_reduce, st.resident_passes, st.resident_giveups)
+
+    def time_exchange(self, depth: int, iters: int = 20) -> tuple:
+        """(seconds per grouped halo exchange of `depth` rows/columns on this
+        rank, its largest message in bytes).  Collective over the ranks."""
+        t = ctypes.c_double()
+        b = ctypes.c_int64()
+        _native.call("heat_solver_time_exchange", self._h, int(depth), int(iters),
+                     ctypes.byref(t), ctypes.byref(b))
+        return t.value, b.value
 
     def reset(self) -> None:
         _native.call("heat_solver_reset", self._h)

@@ -54,34 +54,43 @@ def run_group(config: HeatConfig, world: int, fn: Callable[[HeatSolver], object]
     results: List[object] = [None] * world
     errors: List[Optional[BaseException]] = [None] * world
     solvers: List[Optional[HeatSolver]] = [None] * world
-    lock = threading.Lock()
+    # One lock per rank guards that rank's slot for the whole of an abort: a
+    # rank clears its slot (under its lock) before its solver is closed, so
+    # an abort from a failing peer never runs on a solver being destroyed
+    # (ctypes drops the GIL in both native calls).
+    locks = [threading.Lock() for _ in range(world)]
 
     def fail_peers(rank: int) -> None:
         # Unblock the peers, which would wait forever for this rank's
         # messages: loopback peers raise "a peer rank failed"; RCCL peers have
-        # their communicators aborted (their waits raise "run aborted").
+        # their communicators aborted (their waits raise "run aborted").  The
+        # native abort takes no lock a blocked peer call holds.
         if hub is not None:
             hub.fail()
             return
-        with lock:
-            peers = [s for r, s in enumerate(solvers) if s is not None and r != rank]
-        for s in peers:
-            try:
-                s.abort()
-            except Exception:  # noqa: BLE001 - best effort
-                pass
+        for r in range(world):
+            if r == rank:
+                continue
+            with locks[r]:
+                s = solvers[r]
+                if s is None:
+                    continue
+                try:
+                    s.abort()
+                except Exception:  # noqa: BLE001 - best effort
+                    pass
 
     def body(rank: int) -> None:
         try:
             info = pcomm.DistInfo(rank, world, rank)
             with HeatSolver(config, transport=kind, dist_info=info, device=devices[rank],
                             hub=hub, rccl_uid=uid) as s:
-                with lock:
+                with locks[rank]:
                     solvers[rank] = s
                 try:
                     results[rank] = fn(s)
                 finally:
-                    with lock:
+                    with locks[rank]:
                         solvers[rank] = None
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             errors[rank] = e

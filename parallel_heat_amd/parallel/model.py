@@ -82,9 +82,40 @@ def _grid(cfg: HeatConfig, world: int) -> tuple:
     return d[0], d[1]
 
 
-def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8) -> Dict:
+def fit_exchange(points: Sequence[tuple], base: Dict = None) -> Dict:
+    """Exchange parameters from measured (message bytes, seconds per grouped
+    exchange) points on the real ranks (``HeatSolver.time_exchange``, max over
+    ranks): latency = intercept, link_gbps = 1 / slope of a least-squares line
+    (one point: the stated bandwidth, latency = the rest).  Returns a copy of
+    `base` (default XGMI) with those two replaced and the points attached."""
+    out = dict(base or XGMI)
+    pts = [(float(b), float(t)) for b, t in points if t > 0]
+    if not pts:
+        return out
+    if len(pts) >= 2 and max(b for b, _ in pts) > min(b for b, _ in pts):
+        n = len(pts)
+        mb = sum(b for b, _ in pts) / n
+        mt = sum(t for _, t in pts) / n
+        sxx = sum((b - mb) ** 2 for b, _ in pts)
+        slope = sum((b - mb) * (t - mt) for b, t in pts) / sxx
+        lat = mt - slope * mb
+        if slope > 0:
+            out["link_gbps"] = round(1.0 / slope / 1e9, 3)
+        out["latency_us"] = round(max(lat, 0.0) * 1e6, 3)
+    else:
+        b, t = pts[0]
+        out["latency_us"] = round(max(t - b / (out["link_gbps"] * 1e9), 0.0) * 1e6, 3)
+    out["measured"] = [[int(b), round(t * 1e6, 3)] for b, t in pts]
+    return out
+
+
+def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
+            xgmi: Dict = None) -> Dict:
     """Predicted time per 1000 iterations and node throughput of cfg on
-    `world` GPUs (the slowest rank: the largest block, with neighbours)."""
+    `world` GPUs (the slowest rank: the largest block, with neighbours).
+    `xgmi`: exchange parameters (default the stated XGMI; fit_exchange gives
+    measured ones)."""
+    X = xgmi or XGMI
     px, py = _grid(cfg, world)
     lx = math.ceil(cfg.nx / px)
     ly = math.ceil(cfg.ny / py)
@@ -107,8 +138,8 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8) 
     ns_bytes = H * (ly + 2 * H) * 4 if px > 1 else 0
     ew_bytes = lx * H * 4 if py > 1 else 0
     msg = max(ns_bytes, ew_bytes)
-    t_ex = (XGMI["latency_us"] * 1e-6 + msg / (XGMI["link_gbps"] * 1e9) +
-            (2 * XGMI["pack_us"] * 1e-6 if py > 1 else 0.0))
+    t_ex = (X["latency_us"] * 1e-6 + msg / (X["link_gbps"] * 1e9) +
+            (2 * X["pack_us"] * 1e-6 if py > 1 else 0.0))
     ex_total = exchanges * t_ex
     if schedule != "sync" and world > 1:
         # Overlap schedules: one K-deep exchange per pass, hidden behind the
@@ -120,7 +151,7 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8) 
         compute_s = passes * (max(per_pass, t_ex) + 25e-6)
         ex_total = 0.0
     checks = math.floor(1000 / cfg.check_interval) if cfg.converge else 0
-    reduce_s = checks * XGMI["allreduce_us"] * 1e-6 if world > 1 else 0.0
+    reduce_s = checks * X["allreduce_us"] * 1e-6 if world > 1 else 0.0
     total = compute_s + ex_total + reduce_s
     return {
         "layout": f"{px}x{py}", "block": f"{lx}x{ly}", "schedule": schedule,
@@ -135,16 +166,17 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8) 
     }
 
 
-def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3) -> List[HeatConfig]:
+def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3,
+          xgmi: Dict = None) -> List[HeatConfig]:
     """The candidates whose predicted time is within `slack` x the best
-    prediction (the autotune times only these)."""
+    prediction (the autotune times only these); `xgmi` as in predict."""
     if len(cands) <= 1:
         return list(cands)
-    t = [predict(c, world)["ms_per_1000"] for c in cands]
+    t = [predict(c, world, xgmi=xgmi)["ms_per_1000"] for c in cands]
     best = min(t)
     return [c for c, x in zip(cands, t) if x <= slack * best]
 
 
-def model_params() -> Dict:
-    return {"xgmi": dict(XGMI), "rate_points": [list(p) for p in RATE_POINTS],
+def model_params(xgmi: Dict = None) -> Dict:
+    return {"xgmi": dict(xgmi or XGMI), "rate_points": [list(p) for p in RATE_POINTS],
             "strip_cols": STRIP_COLS, "simds": SIMDS}

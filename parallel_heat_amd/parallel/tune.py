@@ -66,24 +66,57 @@ def describe(cfg: HeatConfig, world: int) -> Dict[str, object]:
     return {"px": px, "py": py, "schedule": cfg.schedule, "halo_passes": cfg.halo_passes}
 
 
+def measure_exchange(solver, depths: Sequence[int], iters: int = 20,
+                     agree_max: Optional[Callable[[float], float]] = None) -> List[tuple]:
+    """(largest message bytes, seconds per grouped exchange) of `solver`'s halo
+    exchange at each depth (<= its halo), timed on the real ranks; `agree_max`
+    reduces a float to its max over the ranks (the slowest rank sets the
+    pace).  Collective.  Feed the points to parallel.model.fit_exchange."""
+    out = []
+    for d in depths:
+        d = max(1, min(int(d), solver.info.halo))
+        t, b = solver.time_exchange(d, iters)
+        if agree_max is not None:
+            t = agree_max(t)
+        out.append((b, t))
+    return out
+
+
+def is_clean_failure(e: BaseException) -> bool:
+    """A run-time failure after which the rank's queued work completed and its
+    communicator was kept (the native run() says "[clean]"): every rank meets
+    it at the same point, so the ranks can agree and go on."""
+    return "[clean]" in str(e)
+
+
 def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConfig]] = None,
              steps: int = 1000, repeats: int = 3,
              make: Optional[Callable[[HeatConfig], object]] = None,
              log: Optional[Callable[[str], None]] = None,
-             shared=None) -> Tuple[HeatConfig, List[dict]]:
+             shared=None, vote_timeout_s: float = 180.0) -> Tuple[HeatConfig, List[dict]]:
     """Time every candidate (steps x repeats, after one untimed run of `steps`
     that captures the graphs) and return (fastest config, table).
 
     `make(cfg)` builds the solver (default: HeatSolver(cfg, dist_info=info,
     shared=shared)); pass `shared` (a parallel.comm.EngineTransport) so every
     candidate rides the same communicator instead of one ncclCommInitRank per
-    candidate.  Collective over torch.distributed's default group when
-    info.world > 1: every rank takes the same sequence of agreements, so a
-    candidate that any rank rejects at construction is skipped on all
-    of them together instead of leaving the ranks in mismatched collectives.
-    That holds for failures at construction only: a candidate that fails
-    while it runs aborts the (shared) transport and the whole autotune on
-    that rank (NativeError); its peers end in their watchdog."""
+    candidate.  Collective over torch.distributed when info.world > 1: the
+    ranks agree after construction, after the untimed run and after the timed
+    runs (a gloo group with a `vote_timeout_s` timeout), so a candidate is
+    skipped on every rank together when any rank
+
+    * rejects it at construction,
+    * fails at run time "cleanly" (the native run() drained its queued work
+      and kept the communicator: a planning check or a non-finite residual,
+      which every rank meets at the same point), or
+    * reports a resident-tile give-up (HEAT_TB_RES_GIVEUP=defer: the run's
+      results are invalid, its transport calls all matched).
+
+    Any other run-time failure aborts the transport and the autotune (its
+    peers may be waiting inside a send/recv that will never match); so does
+    an agreement that times out (a peer stuck in such a wait)."""
+    import datetime
+
     import torch
     import torch.distributed as dist
 
@@ -97,12 +130,18 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             return HeatSolver(c, dist_info=info, shared=shared)
 
     gpu = cfg.backend == "hip"
+    # Agreements go over a gloo group with a timeout: a rank whose peer is
+    # stuck in an engine collective gives up instead of waiting forever.
+    group = None
+    if world > 1:
+        group = dist.new_group(backend="gloo",
+                               timeout=datetime.timedelta(seconds=vote_timeout_s))
 
     def agree_all(flag: float, op) -> float:
         if world == 1:
             return flag
-        t = torch.tensor([flag], dtype=torch.float64, device="cuda" if gpu else "cpu")
-        dist.all_reduce(t, op=op)
+        t = torch.tensor([flag], dtype=torch.float64)
+        dist.all_reduce(t, op=op, group=group)
         return float(t.item())
 
     MIN = dist.ReduceOp.MIN if world > 1 else None
@@ -112,12 +151,53 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
         if gpu:
             torch.cuda.synchronize()
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
     table: List[dict] = []
     best, best_ms = None, float("inf")
+
+    def attempt(solver, row, fn):
+        """Run fn(); returns 1.0, or 0.0 after a clean failure / a resident
+        give-up (recorded in row); raises after any other failure."""
+        try:
+            gave_up = fn()
+            if gave_up:
+                row["error"] = "resident tiles gave up a neighbour wait (results invalid)"
+                return 0.0
+            return 1.0
+        except _native.NativeError as e:
+            if is_clean_failure(e):
+                row["error"] = str(e).splitlines()[0][:200]
+                return 0.0
+            # Peers may be inside a send / recv / all-reduce that will never
+            # match, with unmatched ops queued on the shared communicator: no
+            # later candidate may use it.  Abort it (their pending waits end
+            # in their watchdog, HEAT_WATCHDOG_S) and end the autotune.
+            try:
+                solver.abort()
+            finally:
+                solver.close()
+            raise _native.NativeError(
+                f"autotune aborted: candidate {row} failed at run time on rank "
+                f"{info.rank}: {str(e).splitlines()[0][:200]}") from e
+
+    def agree_ok(solver, row, ok: float) -> bool:
+        try:
+            ok = agree_all(ok, MIN)
+        except RuntimeError as e:  # the gloo agreement timed out
+            try:
+                solver.abort()
+            finally:
+                solver.close()
+            raise _native.NativeError(f"autotune aborted: ranks did not agree on {row}: {e}") \
+                from e
+        if ok < 1.0:
+            solver.close()
+            row.setdefault("error", "failed on another rank")
+            table.append(row)
+            if log:
+                log(f"autotune: {row} skipped")
+            return False
+        return True
+
     for c in candidates:
         row = describe(c, world)
         solver = None
@@ -135,31 +215,27 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             if log:
                 log(f"autotune: {row} skipped")
             continue
-        dt = 0.0
-        try:
-            solver.run(steps)  # graph capture, RCCL connections
-            barrier()
-            sync()
-            t0 = time.perf_counter()
+        # Untimed run (graph capture, RCCL connections); the agreement after
+        # it is also the barrier before the timed runs.
+        ok = attempt(solver, row, lambda: solver.run(steps).resident_giveups > 0)
+        if not agree_ok(solver, row, ok):
+            continue
+        sync()
+        t0 = time.perf_counter()
+
+        def timed():
+            g = 0
             for _ in range(repeats):
-                solver.run(steps)
-            sync()
-            dt = time.perf_counter() - t0
-            row["halo"] = solver.info.halo
-            row["tb_depth"] = solver.info.tb_depth
-        except _native.NativeError as e:
-            # A run-time failure can leave this rank's peers inside a send /
-            # recv / all-reduce that will never match, and unmatched ops queued
-            # on the shared communicator: no later candidate may use it.
-            # Abort it (ncclCommAbort: the peers' pending waits end in their
-            # watchdog, HEAT_WATCHDOG_S) and end the whole autotune.
-            try:
-                solver.abort()
-            finally:
-                solver.close()
-            raise _native.NativeError(
-                f"autotune aborted: candidate {row} failed at run time on rank "
-                f"{info.rank}: {str(e).splitlines()[0][:200]}") from e
+                g += solver.run(steps).resident_giveups
+            return g > 0
+
+        ok = attempt(solver, row, timed)
+        sync()
+        dt = time.perf_counter() - t0
+        if not agree_ok(solver, row, ok):
+            continue
+        row["halo"] = solver.info.halo
+        row["tb_depth"] = solver.info.tb_depth
         solver.close()
         dt = agree_all(dt, MAX)
         ms = dt * 1e3 * 1000.0 / (steps * repeats)
@@ -170,6 +246,8 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             log(f"autotune: {row}")
         if ms < best_ms:
             best, best_ms = c, ms
+    if group is not None:
+        dist.destroy_process_group(group)
     if best is None:
         raise _native.NativeError("autotune: every candidate was rejected: %r" % table)
     return best, table

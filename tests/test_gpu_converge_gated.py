@@ -82,6 +82,25 @@ def test_gated_single_step_kernels(gpu, kernel):
     assert np.array_equal(g, c)
 
 
+@pytest.mark.parametrize("interval,check", [(10, 1), (11, 1), (9, 1), (50, 5)])
+def test_gated_replay_deep_level(gpu, interval, check):
+    # A converging check at level 9, 10 or 11 of a depth-12 pass (every 10
+    # steps: level 10 of pass [0, 12); every 50: step 250 at level 10 of
+    # [240, 252)) on a level-split plate: the replay runs those steps as
+    # passes tb_step takes (rl mod 8, then 8), not as one depth-10 pass.
+    base = HeatConfig(nx=2048, ny=8192, steps=0, converge=True, check_interval=interval,
+                      eps=0.0, init="random", seed=9, backend="cpu", tb_depth=1)
+    with HeatSolver(base) as c:
+        res = [np.float32(c.run(interval).last_resid) for _ in range(check)]
+        want = c.gather()
+    eps = float(np.nextafter(res[-1], np.float32(np.inf)))
+    cfg = base.replace(backend="hip", tb_depth=12, eps=eps)
+    g, r = _run(cfg, 300)
+    assert r.converged and r.converged_at == interval * check, (r.converged_at, res)
+    assert np.float32(r.last_resid) == res[-1]
+    assert np.array_equal(g, want), np.abs(g - want).max()
+
+
 @pytest.mark.parametrize("check", [2, 4])
 def test_gated_split_kernel_check_inside_pass(gpu, check):
     # A plate large enough for the level-split pipelines (>= 64 strip-rows

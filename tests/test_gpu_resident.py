@@ -45,7 +45,7 @@ def test_resident_plate_bitwise(gpu, monkeypatch, nx, ny, steps, fits):
 
 def test_resident_repeated_runs_graph_and_eager(gpu, monkeypatch):
     # bench.py's pattern: the same segment graph replayed (flags re-zeroed by
-    # the memset node every launch), and the eager path.
+    # the last tile of every launch), and the eager path.
     cfg = HeatConfig(nx=1024, ny=8192, steps=0, init="random", seed=3, backend="hip")
     g_graph, rs = _solve(cfg, 0, True, monkeypatch, chunks=[240, 240, 240])
     assert all(r.resident_passes > 0 for r in rs)

@@ -66,15 +66,19 @@ class _FakeSolver:
     per candidate schedule."""
     aborted = []
 
-    def __init__(self, cfg, fail_make=False, fail_run=False):
+    def __init__(self, cfg, fail_make=False, fail_run=False, clean=False, giveup=False):
         if fail_make:
             raise _native.NativeError("block thinner than its halo")
-        self.cfg, self.fail_run = cfg, fail_run
+        self.cfg, self.fail_run, self.clean, self.giveup = cfg, fail_run, clean, giveup
         self.info = type("I", (), {"halo": 12, "tb_depth": 12})()
 
     def run(self, n):
         if self.fail_run:
-            raise _native.NativeError("planner check failed mid-run")
+            # The native run() prefixes "[clean]" when the rank's queued work
+            # completed and the communicator was kept.
+            raise _native.NativeError(("[clean] " if self.clean else "") +
+                                      "planner check failed mid-run")
+        return type("R", (), {"resident_giveups": int(self.giveup)})()
 
     def abort(self):
         _FakeSolver.aborted.append(self.cfg.schedule)
@@ -105,3 +109,81 @@ def test_autotune_aborts_on_a_run_time_failure():
     with pytest.raises(_native.NativeError, match="autotune aborted"):
         _tune({"pipeline": dict(fail_run=True)})
     assert _FakeSolver.aborted == ["pipeline"]
+
+
+def test_autotune_skips_a_clean_run_time_failure():
+    # A failure every rank meets at the same point with the communicator
+    # intact ("[clean]") skips the candidate instead of ending the autotune.
+    _FakeSolver.aborted.clear()
+    best, table = _tune({"pipeline": dict(fail_run=True, clean=True)})
+    assert _FakeSolver.aborted == []
+    assert "[clean]" in table[1]["error"] and "ms_per_1000_iters" not in table[1]
+    assert best.schedule in ("sync", "overlap")
+
+
+def test_autotune_skips_a_resident_giveup():
+    # HEAT_TB_RES_GIVEUP=defer: a run whose resident tiles gave up returns
+    # resident_giveups = 1 (results invalid); the candidate is not timed.
+    _FakeSolver.aborted.clear()
+    best, table = _tune({"sync": dict(giveup=True)})
+    assert "gave up" in table[0]["error"] and _FakeSolver.aborted == []
+    assert best.schedule in ("pipeline", "overlap")
+
+
+def _tune_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    from parallel_heat_amd.parallel.comm import DistInfo
+    from parallel_heat_amd.parallel.tune import autotune
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = HeatConfig(nx=64, ny=64, backend="cpu")
+    cands = [cfg.replace(schedule=s) for s in ("sync", "pipeline", "overlap")]
+    # Rank 1 alone gives up on "sync"; both ranks fail cleanly on "pipeline".
+    fails = {"pipeline": dict(fail_run=True, clean=True)}
+    if rank == 1:
+        fails["sync"] = dict(giveup=True)
+    make = lambda c: _FakeSolver(c, **fails.get(c.schedule, {}))  # noqa: E731
+    best, table = autotune(cfg, DistInfo(rank, world, rank), candidates=cands, steps=2,
+                           repeats=1, make=make)
+    with open(out, "w") as f:
+        f.write(best.schedule + "\n" + "|".join(str("error" in r) for r in table))
+    dist.destroy_process_group()
+
+
+def test_autotune_two_ranks_agree_on_skips(tmp_path):
+    import torch.multiprocessing as mp
+    from .dist_worker import free_port
+    port = free_port()
+    outs = [str(tmp_path / f"r{r}.txt") for r in range(2)]
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_tune_worker, args=(r, 2, port, outs[r])) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    got = [open(o).read().split("\n") for o in outs]
+    assert got[0] == got[1] == ["overlap", "True|True|False"]
+
+
+def test_fit_exchange_and_prune_from_measurements():
+    # Latency and link bandwidth fitted from measured (bytes, seconds) points
+    # replace the stated constants in predict() and prune().
+    from parallel_heat_amd.parallel.model import XGMI, fit_exchange, predict, prune
+    pts = [(3_000_000, 12e-6 + 3_000_000 / 20e9), (750_000, 12e-6 + 750_000 / 20e9)]
+    x = fit_exchange(pts)
+    assert abs(x["link_gbps"] - 20.0) < 0.01 and abs(x["latency_us"] - 12.0) < 0.01
+    assert x["measured"][0] == [3_000_000, round(pts[0][1] * 1e6, 3)]
+    assert XGMI["link_gbps"] == 50.0  # the stated model is untouched
+    one = fit_exchange([(1_000_000, 40e-6)])  # one point: stated GB/s, latency = rest
+    assert abs(one["latency_us"] - 20.0) < 1e-6
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    cands = default_candidates(cfg, 8, schedules=["sync", "pipeline"], halo_passes=[0, 4])
+    p_stated, p_meas = predict(cands[0], 8), predict(cands[0], 8, xgmi=x)
+    assert p_meas["exchange_ms"] > p_stated["exchange_ms"]
+    # Very slow links (1 GB/s) make the 1-D slabs' 3 MB messages the cost:
+    # the 2-D grid's smaller messages win and the slabs are pruned.
+    slow = fit_exchange([(3_000_000, 3_000_000 / 1e9), (750_000, 750_000 / 1e9)])
+    kept = [tuple(describe(c, 8).values()) for c in prune(cands, 8, xgmi=slow)]
+    assert kept and all(k[:2] == (4, 2) for k in kept), kept
