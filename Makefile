@@ -70,9 +70,11 @@ asm:
 	  $(if $(filter tb_scalar tb_split tb_tile,$(ASM)),-fno-slp-vectorize) --offload-device-only -S \
 	  -o $(ASM).s ../../csrc/kernels/$(ASM).hip
 
-resources: $(SRCS_HIP)
-	$(HIPCC) $(HIPFLAGS) -c csrc/kernels/stencil.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \
-	  grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|LDS Size" | paste - - - - - - -
+# Every kernel of every unit, from the built library's code-object metadata
+# (VGPR/AGPR/SGPR, scratch bytes per lane, spilled VGPRs, LDS);
+# tests/test_kernel_resources.py holds the hot kernels to a scratch budget.
+resources: $(LIBDIR)/libheat.so
+	python3 tools/kernel_resources.py $(LIBDIR)/libheat.so
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR)/libheat.so

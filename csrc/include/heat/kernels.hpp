@@ -134,8 +134,8 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
 // (same layout as the field) and per-tile flags.  The tiles of the box must
 // all be co-resident (tb_resident_fits).  src is read by the first pass only;
 // dst receives the last pass's box.  checks: convergence checks inside the
-// launch (increasing passes, at most one per pass, each at the pass's last
-// step: checks[c].step == depth): check c writes the max |delta| of that
+// launch (increasing passes, at most one per pass, each at an even level
+// 2 <= checks[c].step <= depth): check c writes the max |delta| of that
 // step over the owned block [0, own_rows) x [0, own_cols) into
 // resids[slot * kTbResidentMaxChecks + c] (atomic max per wave, 64 slots;
 // words zeroed by the caller, kTbResidentSlots * kTbResidentMaxChecks of

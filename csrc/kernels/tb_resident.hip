@@ -170,7 +170,8 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   HEAT_CHECK(nchecks >= 0 && nchecks <= kResMaxChecks && (nchecks == 0 || resids != nullptr),
              "%d checks in a resident launch (at most %d)", nchecks, kResMaxChecks);
   for (int c = 0; c < nchecks; ++c) {
-    HEAT_CHECK(checks[c].pass >= 0 && checks[c].pass < passes && checks[c].step == depth &&
+    HEAT_CHECK(checks[c].pass >= 0 && checks[c].pass < passes && checks[c].step >= 2 &&
+                   checks[c].step <= depth && checks[c].step % 2 == 0 &&
                    (c == 0 || checks[c].pass > checks[c - 1].pass),
                "resident check %d at pass %d step %d (passes %d, depth %d)", c, checks[c].pass,
                checks[c].step, passes, depth);

@@ -27,8 +27,8 @@ struct ResArgs {
   unsigned* err;        // non-zero: a neighbour wait gave up (bounded spin)
   int64_t own_r1, own_c1;  // owned block [0, own_r1) x [0, own_c1): the residual's cells
   // Convergence checks inside the launch: check c takes the residual of
-  // the LAST step of pass chk_pass[c] into resids[c] (RES 1; chk_step[c]
-  // is K, checked on the host).
+  // level chk_step[c] (even, 2..K; checked on the host) of pass chk_pass[c]
+  // into resids[c] (RES 1).
   int nchk;
   unsigned* resids;
   int chk_pass[kResMaxChecks], chk_step[kResMaxChecks];
@@ -167,26 +167,33 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
             nopub ? false : band_lane, vlane, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
-    // The check of this pass (at most one, at its last step), if any.
+    // The check of this pass (at most one, at an even level), if any.
     int ci = -1;
     if constexpr (RES == 1) {
       for (int c = 0; c < ra.nchk; ++c)
         if (ra.chk_pass[c] == p) ci = c;
     }
-    unsigned rm = ci >= 0 ? resmask : 0u;  // the last step's residual rows
+    int acc_step = ci >= 0 ? ra.chk_step[ci] - 1 : -1;  // its step index (odd: an up step)
+    opaque32(acc_step);
+    unsigned rm = ci >= 0 ? resmask : 0u;  // the check step's residual rows
     opaque(rm);
-    tile_pass_steps<RES == 1 ? 2 : 0, LAST ? 1 : 3>(K, [&](auto down_c, auto what_c, auto acc_c,
-                                                          int s) {
-      constexpr bool D = decltype(down_c)::value;
-      xc.p = s & 1;
-      xc.last_w = xc.next_w = D ? wb : wa;
-      const vecf first_nb = xc.efirst;
-      opaque(rowmask);
-      opaque(usemask);
-      T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-          first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub, rm,
-          res_rc);
-    });
+    tile_pass_steps<RES == 1 ? 3 : 0, LAST ? 1 : 3>(
+        K,
+        [&](auto down_c, auto what_c, auto acc_c, int s) {
+          constexpr bool D = decltype(down_c)::value;
+          xc.p = s & 1;
+          xc.last_w = xc.next_w = D ? wb : wa;
+          const vecf first_nb = xc.efirst;
+          opaque(rowmask);
+          opaque(usemask);
+          // The last step always runs the accumulating body: rows only if
+          // the check is there.
+          const unsigned rms = s == acc_step ? rm : 0u;
+          T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
+              first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub,
+              rms, res_rc);
+        },
+        acc_step);
     if constexpr (RES == 1) {
       if (ci >= 0) {
         const int slot = (u * NW + w) & (kTbResidentSlots - 1);

@@ -146,8 +146,14 @@ __device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, in
 //     take checks at pass ends; the other steps stay free of residual code).
 //     Choosing between two last-step bodies per pass, or a body per check
 //     step, spilled 80-330 B/lane.
+//   ACC_MODE 3: as 2, plus an accumulating UP body inside the loop, taken at
+//     step acc_step (odd: an even level, 2..K-2) by a uniform branch; the
+//     last step is the accumulating body as in mode 2 (the caller zeroes its
+//     row mask unless acc_step == K - 1).  The resident kernel's checks at
+//     inner even levels (depth 12, a check every 20 or 50 steps: levels 8,
+//     4, 12 / 2, 4, ..., 12), so depth 10 is no longer forced on them.
 template <int ACC_MODE, int LAST_WHAT, class StepFn>
-__device__ __forceinline__ void tile_pass_steps(int K, StepFn&& st) {
+__device__ __forceinline__ void tile_pass_steps(int K, StepFn&& st, int acc_step = -1) {
   using Down = std::true_type;
   using Up = std::false_type;
   using Plain = std::integral_constant<int, 0>;
@@ -155,6 +161,21 @@ __device__ __forceinline__ void tile_pass_steps(int K, StepFn&& st) {
   using A = std::integral_constant<bool, ACC_MODE == 1>;
   using AL = std::integral_constant<bool, ACC_MODE != 0>;
   int s = 0;
+  if constexpr (ACC_MODE == 3) {
+    // The pairs before the check's pair, the check's pair, the rest: two
+    // loops of the one plain body around it (a branch between two up
+    // bodies inside one loop spilled 556 B/lane, all of it in the loop).
+    const int q = (acc_step >= 1 && acc_step + 2 < K) ? acc_step - 1 : K;
+    for (; s + 2 < K && s < q; s += 2) {
+      st(Down{}, Plain{}, A{}, s);
+      st(Up{}, Plain{}, A{}, s + 1);
+    }
+    if (s == q) {
+      st(Down{}, Plain{}, A{}, s);
+      st(Up{}, Plain{}, std::true_type{}, s + 1);
+      s += 2;
+    }
+  }
   for (; s + 2 < K; s += 2) {
     st(Down{}, Plain{}, A{}, s);
     st(Up{}, Plain{}, A{}, s + 1);

@@ -331,13 +331,14 @@ int Solver::auto_tb_depth() const {
   int64_t min_lx = INT64_MAX;
   for (int r = 0; r < cart_.world; ++r) min_lx = std::min(min_lx, make_block(cart_, r, P_.nx, P_.ny).lx);
   const int base = min_lx >= 1024 ? gpu::kTbDeepDepth : 8;
-  // Convergence checks every C steps on tile-sized blocks: a depth that
-  // divides C puts every check at the end of a pass, where resident spans
-  // take it without leaving the launch (tb_resident.hip; a check inside a
-  // pass ends the span).  10 for C = 20, 50, 100, ...: 1024 x 8192 checking
-  // every 20 steps ran -21 % with its checks inside depth-12 passes.
-  if (P_.converge && P_.compat != Compat::Cuda && P_.check_interval % base != 0 &&
-      env_int("HEAT_TB_RESIDENT", 1) != 0) {
+  // Convergence checks on tile-sized blocks: resident spans take a check at
+  // any even level of a depth-12 pass (tb_resident_kern.hpp, ACC_MODE 3), so
+  // an even interval (20, 50, ...) keeps depth 12 and its spans; round 4
+  // forced depth 10 there (checks at pass ends only), -5.6 % per pass on
+  // 1024 x 8192.  Odd intervals put every other check at an odd level: a
+  // depth dividing the interval keeps those at pass ends.
+  if (P_.converge && P_.compat != Compat::Cuda && P_.check_interval % 2 != 0 &&
+      P_.check_interval % base != 0 && env_int("HEAT_TB_RESIDENT", 1) != 0) {
     for (int d : {10, 8})
       if (P_.check_interval % d == 0 && tile_sized_at(d)) return d;
   }
@@ -674,8 +675,10 @@ int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
   int n = 0, nchk = 0;
   for (size_t j = i; j < plan.size(); ++j) {
     if (plan[j].k != k) break;
-    // Checks at pass ends only (the resident kernel's residual step).
-    if (plan[j].rl != 0 && (!gated() || plan[j].rl != k || nchk == gpu::kTbResidentMaxChecks))
+    // Checks at even levels (the resident kernel's residual bodies: the up
+    // steps), device-judged runs only.
+    if (plan[j].rl != 0 &&
+        (!gated() || plan[j].rl % 2 != 0 || nchk == gpu::kTbResidentMaxChecks))
       break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
     if (ns) gr -= k;

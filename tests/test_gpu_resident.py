@@ -83,11 +83,11 @@ def test_resident_multirank_deep_halo(gpu, monkeypatch, world, kw):
 
 @pytest.mark.parametrize("interval", [50, 20, 7])
 def test_resident_with_checks(gpu, monkeypatch, interval):
-    # Checks at pass ends ride inside resident spans (the automatic depth
-    # divides the interval: 10 for 20 and 50); a converging check replays the
-    # span from its source buffer.  Every 7 steps the checks fall inside
-    # passes (depth 8: cut passes, no spans).  Converges, bitwise vs the CPU
-    # oracle and vs separate passes.
+    # Checks at even levels ride inside resident spans (every 20 / 50 steps
+    # at depth 8 on this plate: levels 4, 8 / 2, 4, 6, 8); a converging check
+    # replays the span from its source buffer.  Every 7 steps every other
+    # check falls at an odd level (cut passes, no spans).  Converges, bitwise
+    # vs the CPU oracle and vs separate passes.
     cfg = HeatConfig(nx=48, ny=96, steps=40000, converge=True, check_interval=interval,
                      eps=1e-3, init="ref-wrap", backend="hip")
     g1, r1 = _solve(cfg, None, True, monkeypatch)
@@ -100,16 +100,19 @@ def test_resident_with_checks(gpu, monkeypatch, interval):
 
 
 @pytest.mark.parametrize("world,kw,interval,check", [
-    (1, dict(nx=1024, ny=8192), 20, 4),               # depth 10: step 80 ends pass 8 of a span
-    (1, dict(nx=1024, ny=8192), 60, 1),               # depth 12: step 60 ends pass 5
-    (1, dict(nx=1024, ny=8192), 50, 2),               # depth 10: step 100
+    (1, dict(nx=1024, ny=8192), 20, 4),               # depth 12: step 80, level 8 of pass 7
+    (1, dict(nx=1024, ny=8192), 20, 1),               # step 20, level 8 of pass 2 (the 2nd of a span)
+    (1, dict(nx=1024, ny=8192), 20, 3),               # step 60 ends pass 5
+    (1, dict(nx=1024, ny=8192), 50, 2),               # step 100, level 4 of pass 9
+    (1, dict(nx=1024, ny=8192), 50, 5),               # step 250, level 10 of pass 21
     (2, dict(nx=1024, ny=1024, decomp="rows"), 20, 4),  # deep halos: the owned rows only
     (4, dict(nx=1024, ny=1024, px=2, py=2), 50, 1),     # 2-D blocks: owned rows and columns only
 ])
 def test_resident_span_converges_inside(gpu, monkeypatch, world, kw, interval, check):
     # eps just above the CPU oracle's residual at check `check`: the run
-    # converges exactly there, inside or at the end of a resident span, and
-    # its state is the span replayed from its source buffer.
+    # converges exactly there, at an inner even level or at the end of a pass
+    # of a resident span (depth 12 whatever the interval: round 4 forced
+    # depth 10), and its state is the span replayed from its source buffer.
     base = HeatConfig(steps=0, converge=True, check_interval=interval, eps=0.0, init="random",
                       seed=4, backend="cpu", tb_depth=1, nx=kw["nx"], ny=kw["ny"])
     with HeatSolver(base) as c:
@@ -130,6 +133,24 @@ def test_resident_span_converges_inside(gpu, monkeypatch, world, kw, interval, c
         got = next(g for _, g in out if g is not None)
         assert all(o[0].converged_at == r.converged_at for o in out)
     assert r.resident_passes > 0, r
+    if world == 1:
+        with HeatSolver(cfg) as s:
+            assert s.info.tb_depth == 12
     assert r.converged and r.converged_at == interval * check, (r.converged_at, res)
     assert np.float32(r.last_resid) == res[-1]
     assert np.array_equal(got, want), np.abs(got - want).max()
+
+
+@pytest.mark.parametrize("interval", [20, 50])
+def test_resident_inner_checks_not_converging(gpu, monkeypatch, interval):
+    # 1024 x 8192 at depth 12 checking every 20 / 50 steps without converging
+    # (eps 0): every check's residual is taken at its level inside a resident
+    # span (the last one reported), the state bitwise the separate passes'.
+    cfg = HeatConfig(nx=1024, ny=8192, steps=0, converge=True, check_interval=interval,
+                     eps=0.0, init="random", seed=6, backend="hip")
+    g1, r1 = _solve(cfg, 600, True, monkeypatch)
+    g0, r0 = _solve(cfg, 600, False, monkeypatch)
+    assert r1[0].resident_passes > 0 and r0[0].resident_passes == 0
+    assert not r1[0].converged and r1[0].checks == r0[0].checks == 600 // interval
+    assert np.float32(r1[0].last_resid) == np.float32(r0[0].last_resid)
+    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()

@@ -3,6 +3,10 @@
 
     python tools/asm_loops.py build/asm/tb_split.s tb_split_kernelILi12ELi6E [--min 100]
 
+With --scratch, the number of scratch (spill / reload) instructions per loop
+instead: a spill outside every step loop costs little, one inside costs a
+memory round trip per iteration (tests/test_kernel_resources.py, the budget).
+
 A loop is a backward branch (s_cbranch_* / s_branch to an earlier label); its
 body is the text from the target label to the branch.  For each loop with at
 least --min instructions it prints the count per class (VALU arithmetic, DPP,
@@ -45,6 +49,9 @@ def main():
     ap.add_argument("kernel", help="substring of the mangled kernel name")
     ap.add_argument("--min", type=int, default=100)
     ap.add_argument("--other", action="store_true", help="list the valu_other opcodes")
+    ap.add_argument("--scratch", action="store_true",
+                    help="only print the scratch (spill / reload) instructions inside each loop "
+                         "and in the whole kernel")
     a = ap.parse_args()
     lines = open(a.asm).read().splitlines()
     start = next(i for i, l in enumerate(lines)
@@ -52,6 +59,8 @@ def main():
     end = next((i for i in range(start + 1, len(lines)) if re.match(r"^_Z\S*:", lines[i])),
                len(lines))
     body = lines[start:end]
+    if a.scratch:
+        print(f"scratch instructions in the kernel: {sum('scratch_' in l for l in body)}")
     labels = {}
     for i, l in enumerate(body):
         m = re.match(r"^(\.LBB\w+):", l)
@@ -74,6 +83,11 @@ def main():
                 others[op] += 1
         n = sum(cnt.values())
         if n < a.min:
+            continue
+        if a.scratch:
+            sc = sum(1 for l2 in body[labels[m.group(2)]:i + 1] if "scratch_" in l2)
+            print(f"loop {m.group(2)} (lines {start + labels[m.group(2)] + 1}-{start + i + 1}): "
+                  f"{n} instrs, {sc} scratch")
             continue
         print(f"loop {m.group(2)} (lines {start + labels[m.group(2)] + 1}-{start + i + 1}): {n} instrs")
         for k, v in sorted(cnt.items(), key=lambda kv: -kv[1]):
