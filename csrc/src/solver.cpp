@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <thread>
 
 #include "heat/common.hpp"
@@ -655,13 +656,16 @@ gpu::StencilGeom Solver::geom() const {
 }
 
 int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
-  if (!resident_ || plan[i].k != T_) return 0;
+  // Passes of the configured depth, or a run of equal even remainder passes
+  // (1000 steps at depth 12 end in 8 + 8: one 2-pass launch instead of two
+  // tile launches that each load and store the whole block).
+  if (!resident_ || plan[i].k < 4 || plan[i].k % 2 != 0 || plan[i].k > T_) return 0;
   // Checks may end any pass of a span (device-judged runs: each residual goes
   // to its own word, judged in order after the launch; replay_check re-runs
   // the span up to a converging one).
   if (tr_->world() > 1 && !resident_force_ && device_users(P_.device >= 0 ? P_.device : 0) > 1)
     return 0;
-  const int k = T_;
+  const int k = plan[i].k;
   const bool ns = cart_.px > 1, ew = cart_.py > 1;
   // Ghost validity after the first pass's (possible) exchange, then the
   // bookkeeping of ensure_ghosts pass by pass: the span ends before a pass
@@ -1179,7 +1183,12 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   const int64_t C = P_.check_interval;
   // ~512 steps per segment, a whole number of check periods: every segment
   // of a run starts at the same check phase (one graph per shape).
-  const int64_t seg_cap = C * std::max<int64_t>(1, (512 + C - 1) / C);
+  // Segments of a whole number of lcm(C, T) steps where that is at most
+  // 1024 (20 and 12: 540 steps, 45 full passes; a plain multiple of C left
+  // a remainder pair of depth-8 passes in every segment), else of C.
+  const int64_t L = std::lcm<int64_t>(C, std::max(1, T_));
+  const int64_t unit = L <= 1024 ? L : C;
+  const int64_t seg_cap = unit * std::max<int64_t>(1, (512 + unit - 1) / unit);
   auto* gate_h = static_cast<gpu::DeviceGate*>(h_gate_);
   HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(gpu::DeviceGate), s_comp_));
   HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
