@@ -292,13 +292,20 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
+    # Plain runs are enqueued back to back (HeatSolver.run(wait=False)): the
+    # device goes from one 1000-iteration step to the next without a host
+    # round trip in between; run(0) completes them (and reports errors).
+    # Convergence checks and phase timing run step by step.
+    wait = args.converge or args.phase_timing
+
     def measure():
         """Warmup, then the timed region.  None if a resident launch gave up
         on any rank (the ranks agree outside the timed region)."""
         watchdog("warmup", args.watchdog_s)
         gave = 0
         for _ in range(args.warmup):
-            gave += solver.run(args.iters_per_step).resident_giveups
+            gave += solver.run(args.iters_per_step, wait=wait).resident_giveups
+        gave += solver.run(0).resident_giveups
         if not vote(gave == 0):
             return None
         barrier()
@@ -308,10 +315,11 @@ def main() -> int:
         done = 0
         phases = [0.0, 0.0, 0.0]
         for _ in range(args.steps):
-            r = solver.run(args.iters_per_step)
+            r = solver.run(args.iters_per_step, wait=wait)
             done += r.steps_done
             gave += r.resident_giveups
             phases = [phases[0] + r.t_exchange, phases[1] + r.t_compute, phases[2] + r.t_reduce]
+        gave += solver.run(0).resident_giveups
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0

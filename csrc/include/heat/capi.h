@@ -112,6 +112,9 @@ int heat_transport_info_get(heat_transport* t, heat_transport_info* out);
 int heat_solver_create_shared(const heat_params* p, heat_transport* t, heat_solver** out);
 int heat_solver_destroy(heat_solver* s);
 int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
+/* Asynchronous run (plain GPU runs): enqueue the steps and return; the next
+   heat_solver_run (steps 0: just complete) waits for them and checks errors. */
+int heat_solver_enqueue(heat_solver* s, int64_t steps, heat_run_stats* out);
 /* RCCL on one rank: self send/recv (eager or hipGraph-captured) + all-reduce. */
 int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double* gbps);
 /* Loopback transport: ranks are threads of this process sharing one hub. */

@@ -152,7 +152,7 @@ struct TbResidentBuffers {
 struct TbResidentCheck {
   int pass = 0, step = 0;
 };
-constexpr int kTbResidentMaxChecks = 32;
+constexpr int kTbResidentMaxChecks = 64;  // a 1024-step gated segment checking every 20 steps: 51
 bool tb_resident_fits(const Box& box, int depth, int variant = -1);
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,
                       int depth, int passes, const TbResidentBuffers& xb, hipStream_t st,

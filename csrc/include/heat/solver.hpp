@@ -77,6 +77,13 @@ class Solver {
   // queued collectives would otherwise wait for peers forever (and the
   // destructor's device syncs with them).
   RunStats run(int64_t steps);
+  // Asynchronous run: enqueues the steps and returns (steps_done set, no
+  // timing); the next run() -- run(0) to just complete -- waits for every
+  // enqueued step, checks the resident error word and the transport, and
+  // reports a give-up.  Back-to-back enqueues keep the device busy across
+  // calls (bench.py's timed loop).  Runs that must sync (device-gated
+  // checks, phase timing, host-staged exchanges) are synchronous anyway.
+  RunStats enqueue(int64_t steps);
   // Seconds per grouped halo exchange of `depth` rows/columns (device time
   // over `iters` back-to-back exchanges, this rank); *max_bytes: the largest
   // message.  Collective.  Feeds the autotune's exchange model.
@@ -175,7 +182,9 @@ class Solver {
   int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
   static int device_users(int dev);  // live GPU solvers of this process on dev
   void enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int n);
-  RunStats run_impl(int64_t steps);
+  RunStats run_impl(int64_t steps, bool wait);
+  RunStats run_guarded(int64_t steps, bool wait);
+  void complete_pending();  // run(0) if an enqueue()d run is in flight
   gpu::StencilGeom geom() const;
   void exchange(int buf, int k, hipStream_t st);
   // `st`: the stream to launch on (nullptr = the compute stream).
@@ -222,6 +231,7 @@ class Solver {
   bool resident_ = false;  // resident-tile launches enabled for this solver
   bool resident_force_ = false;  // HEAT_TB_RESIDENT=2: also with ranks sharing the device
   bool resident_used_ = false;  // one was enqueued in this run (check its error word)
+  bool pending_ = false;         // an enqueue()d run not yet completed by run()
   bool defer_giveup_ = false;   // HEAT_TB_RES_GIVEUP=defer: report a give-up, do not throw
   bool inject_giveup_ = false;  // HEAT_TEST_RES_GIVEUP_RANK: fake one give-up (tests)
   float* xbase_[2] = {nullptr, nullptr};  // their exchange fields

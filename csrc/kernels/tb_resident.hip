@@ -181,6 +181,13 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   ra.nchk = nchecks;
   ra.resids = resids;
   a.resid = nchecks > 0 ? resids : nullptr;  // selects the RES 1 instantiation
+  // Timing diagnostic: the RES 1 build without checks (what the residual
+  // instantiation costs by itself, profiles/r5_resident_checks.md).
+  static const bool diag_res1 = [] {
+    const char* e = std::getenv("HEAT_TB_RES_DIAG_RES1");
+    return e && *e && *e != '0';
+  }();
+  if (diag_res1 && resids) a.resid = resids;
   a.res_level = depth;
   a.g = g;
   a.flags = (variant < 0 || (variant & tbv::kXcdGroups)) ? tbdetail::kTbXcdGroups : 0;

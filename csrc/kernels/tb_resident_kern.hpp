@@ -54,9 +54,10 @@ __device__ __forceinline__ void wave_max_atomic_u(float m, unsigned* word) {
 }
 
 // RES 1: the residuals of the checks inside the launch (ResArgs::chk_*),
-// each at the last step of its pass (tile_pass_steps ACC_MODE 2); each
-// wave's max goes to the check's word of its slot at the end of that pass.  A
-// separate instantiation: the RES 0 kernel keeps its register allocation.
+// each at an even level of its pass (tile_pass_steps ACC_MODE 3); each
+// wave's max goes to the check's word of its slot after the next pass's
+// ghost loads (the last pass: at its end).  A separate instantiation: the
+// RES 0 kernel keeps its register allocation.
 template <int R, int NW, int MODE, int XL, int RES>
 __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx, int strip, int t,
                                              int u, vecf (*xch)[2][NW][64]) {
@@ -151,6 +152,19 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     }
   };
 
+  // A check's wave max waiting for its atomic (RES 1).
+  float pend_m = 0.f;
+  int pend_c = -1;
+  auto flush_resid = [&]() {
+    if constexpr (RES == 1) {
+      if (pend_c >= 0) {
+        const int slot = (u * NW + w) & (kTbResidentSlots - 1);
+        wave_max_atomic_u(pend_m, ra.resids + slot * kResMaxChecks + pend_c);
+        pend_c = -1;
+      }
+    }
+  };
+
   // One pass: LDS slots of the fictional step -1, then K steps; the last one
   // publishes the edge bands (LAST false) or stores the box to dst (LAST).
   auto pass = [&](auto last_c, int p) {
@@ -196,9 +210,14 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
         acc_step);
     if constexpr (RES == 1) {
       if (ci >= 0) {
-        const int slot = (u * NW + w) & (kTbResidentSlots - 1);
-        wave_max_atomic_u(T.m, ra.resids + slot * kResMaxChecks + ci);
+        // Deferred: the atomic goes out after the next pass's ghost loads
+        // (refill), not in front of the publish's vmcnt(0) drain, where ~63
+        // atomics per residual word (4032 waves, 64 slots) held every check
+        // pass's boundary; the last pass issues it at once.
+        pend_m = T.m;
+        pend_c = ci;
         T.m = 0.f;
+        if constexpr (LAST) flush_resid();
       }
     }
   };
@@ -226,7 +245,10 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       }
     }
     __syncthreads();
-    if (ra.diag & 2) return;
+    if (ra.diag & 2) {
+      flush_resid();
+      return;
+    }
     const __amdgpu_buffer_rsrc_t rs = xr[(p - 1) & 1];
     unsigned gm = ghostmask, um = usemask;
     opaque(gm);
@@ -241,6 +263,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
       if ((full && box_lane) || (part && ghost_lane))
         T.u[r] = __builtin_bit_cast(vecf, __builtin_amdgcn_raw_buffer_load_b128(rs, vlane, xr0 + r * xp, 16));
     }
+    flush_resid();  // behind the ghost loads: their waits do not include it
   };
 
   const int P = ra.passes;

@@ -265,25 +265,36 @@ int heat_solver_destroy(heat_solver* s) {
   return guard([&] { delete s; });
 }
 
+namespace {
+void fill_stats(const heat::RunStats& r, heat_run_stats* out) {
+  out->steps_done = r.steps_done;
+  out->total_steps = r.total_steps;
+  out->converged = r.converged;
+  out->converged_at = r.converged_at;
+  out->last_resid = r.last_resid;
+  out->seconds = r.seconds;
+  out->t_exchange = r.t_exchange;
+  out->t_compute = r.t_compute;
+  out->t_reduce = r.t_reduce;
+  out->passes = r.passes;
+  out->exchanges = r.exchanges;
+  out->checks = r.checks;
+  out->resident_passes = r.resident_passes;
+  out->resident_giveups = r.resident_giveups;
+}
+}  // namespace
+
+int heat_solver_enqueue(heat_solver* s, int64_t steps, heat_run_stats* out) {
+  return guard([&] {
+    const heat::RunStats r = s->s->enqueue(steps);
+    if (out) fill_stats(r, out);
+  });
+}
+
 int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out) {
   return guard([&] {
-    heat::RunStats r = s->s->run(steps);
-    if (out) {
-      out->steps_done = r.steps_done;
-      out->total_steps = r.total_steps;
-      out->converged = r.converged;
-      out->converged_at = r.converged_at;
-      out->last_resid = r.last_resid;
-      out->seconds = r.seconds;
-      out->t_exchange = r.t_exchange;
-      out->t_compute = r.t_compute;
-      out->t_reduce = r.t_reduce;
-      out->passes = r.passes;
-      out->exchanges = r.exchanges;
-      out->checks = r.checks;
-      out->resident_passes = r.resident_passes;
-      out->resident_giveups = r.resident_giveups;
-    }
+    const heat::RunStats r = s->s->run(steps);
+    if (out) fill_stats(r, out);
   });
 }
 

@@ -313,7 +313,10 @@ void Solver::init_fields() {
   gr_ = gc_ = 0;
 }
 
-void Solver::reset() { init_fields(); }
+void Solver::reset() {
+  complete_pending();
+  init_fields();
+}
 
 int64_t Solver::configured_steps(int64_t steps) const {
   return P_.compat == Compat::Mpi ? steps + 1 : steps;
@@ -1184,11 +1187,14 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   // ~512 steps per segment, a whole number of check periods: every segment
   // of a run starts at the same check phase (one graph per shape).
   // Segments of a whole number of lcm(C, T) steps where that is at most
-  // 1024 (20 and 12: 540 steps, 45 full passes; a plain multiple of C left
-  // a remainder pair of depth-8 passes in every segment), else of C.
+  // 1024 (20 and 12: 60-step units; a plain multiple of C left a remainder
+  // pair of depth-8 passes in every segment), else of C, about 1024 steps
+  // long: a 1000-step run is one segment (one graph, one resident span
+  // with up to kTbResidentMaxChecks checks, one judge); ~512-step segments
+  // cost the 1024 x 8192 plate 2 % at a check every 100 steps.
   const int64_t L = std::lcm<int64_t>(C, std::max(1, T_));
   const int64_t unit = L <= 1024 ? L : C;
-  const int64_t seg_cap = unit * std::max<int64_t>(1, (512 + unit - 1) / unit);
+  const int64_t seg_cap = unit * std::max<int64_t>(1, (1024 + unit - 1) / unit);
   auto* gate_h = static_cast<gpu::DeviceGate*>(h_gate_);
   HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(gpu::DeviceGate), s_comp_));
   HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
@@ -1288,10 +1294,25 @@ void Solver::replay_check(const PassRec& p) {
   sync_watch();
 }
 
-RunStats Solver::run(int64_t steps) {
+RunStats Solver::run(int64_t steps) { return run_guarded(steps, true); }
+
+void Solver::complete_pending() {
+  // State access after enqueue(): wait for the enqueued steps first.  A
+  // deferred resident give-up would otherwise go unseen by a caller that
+  // never calls run() again: raise it here.
+  if (!pending_) return;
+  const RunStats r = run(0);
+  HEAT_CHECK(r.resident_giveups == 0,
+             "an enqueued run's resident tiles gave up a neighbour wait: the state is invalid");
+}
+
+RunStats Solver::enqueue(int64_t steps) { return run_guarded(steps, false); }
+
+RunStats Solver::run_guarded(int64_t steps, bool wait) {
   try {
-    return run_impl(steps);
+    return run_impl(steps, wait);
   } catch (const std::exception& e) {
+    pending_ = false;
     if (tr_->world() > 1) {
       if (capturing_) {
         // Drop the half-built capture (its stream is unusable otherwise).
@@ -1332,6 +1353,7 @@ RunStats Solver::run(int64_t steps) {
 }
 
 double Solver::time_exchange(int depth, int iters, int64_t* max_bytes) {
+  complete_pending();
   // One grouped exchange phase of `depth` rows / columns (the message list a
   // run's deep-halo exchange sends), timed on the device over `iters`
   // back-to-back phases after one untimed phase (RCCL connections).  A halo
@@ -1358,12 +1380,21 @@ double Solver::time_exchange(int depth, int iters, int64_t* max_bytes) {
   return 1e-3 * double(ms) / iters;
 }
 
-RunStats Solver::run_impl(int64_t steps) {
+RunStats Solver::run_impl(int64_t steps, bool wait) {
   TraceRange trace("heat.run");
   RunStats s;
   HEAT_CHECK(steps >= 0, "negative step count");
   const int64_t p0 = stat_passes_, e0 = stat_exchanges_, res0 = stat_resident_;
-  synchronize();
+  // An enqueued run (enqueue) still in flight: continue its stream; its
+  // error word and transport are checked when this call completes.
+  const bool cont = pending_;
+  if (!cont) {
+    synchronize();
+    resident_used_ = false;
+  }
+  // Only plain GPU runs are asynchronous: gated runs read the device gate
+  // on the host, phase timing syncs per phase, host-staged exchanges block.
+  if (!on_gpu() || gated() || timing_ || staged_) wait = true;
   const double t0 = now_s();
   const bool gpu = on_gpu();
   if (timing_) {
@@ -1380,11 +1411,19 @@ RunStats Solver::run_impl(int64_t steps) {
     sync_watch();
     warmed_ = true;
   }
-  resident_used_ = false;
   if (steps > 0) {
     if (gated()) run_gated(steps, s);
     else run_segments(steps, s);
   }
+  if (!wait) {
+    pending_ = true;
+    s.total_steps = step_;
+    s.passes = stat_passes_ - p0;
+    s.exchanges = stat_exchanges_ - e0;
+    s.resident_passes = stat_resident_ - res0;
+    return s;
+  }
+  pending_ = false;
   unsigned* d_err = resident_used_ ? d_flags_ + kResidentFlagBytes / 4 : nullptr;
   if (d_err) HIP_CHECK(hipMemcpyAsync(h_err_, d_err, 4, hipMemcpyDeviceToHost, s_comp_));
   sync_watch();
@@ -1515,6 +1554,7 @@ void Solver::synchronize() {
 // state access, gather, checksum, binary I/O
 // ---------------------------------------------------------------------------
 void Solver::copy_owned(float* host, int64_t host_pitch) {
+  complete_pending();
   if (on_gpu()) {
     HIP_CHECK(hipMemcpy2DAsync(host, size_t(host_pitch) * 4, field_[cur_], size_t(L_.pitch) * 4,
                                size_t(blk_.ly) * 4, size_t(blk_.lx), hipMemcpyDeviceToHost,
@@ -1527,6 +1567,7 @@ void Solver::copy_owned(float* host, int64_t host_pitch) {
 }
 
 void Solver::load_owned(const float* host, int64_t host_pitch, int64_t step) {
+  complete_pending();
   synchronize();
   for (int b = 0; b < 2; ++b) {
     if (on_gpu()) {
@@ -1544,6 +1585,7 @@ void Solver::load_owned(const float* host, int64_t host_pitch, int64_t step) {
 }
 
 void Solver::scatter_root(const float* full, int64_t step) {
+  complete_pending();
   TraceRange tr("heat.scatter");
   const int rank = tr_->rank(), world = tr_->world();
   const bool dev = tr_->device_memory();
@@ -1594,6 +1636,7 @@ void Solver::scatter_root(const float* full, int64_t step) {
 }
 
 std::vector<float> Solver::gather_root() {
+  complete_pending();
   TraceRange trace("heat.gather");
   const int rank = tr_->rank(), world = tr_->world();
   std::vector<float> mine(static_cast<size_t>(blk_.lx * blk_.ly));
@@ -1667,6 +1710,7 @@ void Solver::reduce_scalars(double* f64, int nf, uint64_t* u64, int nu, float* f
 }
 
 Checksum Solver::checksum() {
+  complete_pending();
   TraceRange tr("heat.checksum");
   Checksum c;
   if (on_gpu()) {
@@ -1702,6 +1746,7 @@ Checksum Solver::checksum() {
 }
 
 void Solver::write_bin(const std::string& path) {
+  complete_pending();
   TraceRange trace("heat.output");
   // Written as `path`.tmp by every rank, then renamed by rank 0 once all
   // blocks are in: a crash mid-write (a --checkpoint-every run) leaves the
@@ -1730,6 +1775,7 @@ void Solver::write_bin(const std::string& path) {
 }
 
 void Solver::read_bin(const std::string& path) {
+  complete_pending();
   TraceRange trace("heat.resume");
   BinHeader h = bin_read_header(path);
   HEAT_CHECK(h.nx == P_.nx && h.ny == P_.ny, "checkpoint is %lldx%lld, run is %lldx%lld",

@@ -129,6 +129,7 @@ _SIGS = {
     "heat_transport_info_get": (c_int, [c_void_p, POINTER(HeatTransportInfo)]),
     "heat_solver_create_shared": (c_int, [POINTER(HeatParams), c_void_p, POINTER(c_void_p)]),
     "heat_solver_run": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
+    "heat_solver_enqueue": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
     "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
     "heat_rccl_self_test": (c_int, [c_int, c_int64, c_int, c_int, POINTER(c_double)]),
     "heat_loopback_hub_destroy": (c_int, [c_void_p]),

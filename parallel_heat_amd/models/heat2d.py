@@ -180,12 +180,19 @@ class HeatSolver:
         return self.info.world
 
     # -- running ----------------------------------------------------------------
-    def run(self, steps: Optional[int] = None) -> RunResult:
-        """Advance `steps` steps (default: the config's full run, minus steps done)."""
+    def run(self, steps: Optional[int] = None, wait: bool = True) -> RunResult:
+        """Advance `steps` steps (default: the config's full run, minus steps done).
+
+        wait=False enqueues them and returns at once (plain GPU runs; gated
+        convergence checks, phase timing and host-staged halos still wait):
+        back-to-back calls keep the device busy, and the next run() -- run(0)
+        to just complete -- waits for every enqueued step and reports
+        errors and resident give-ups.  seconds is 0 for an enqueued run."""
         if steps is None:
             steps = self.config.total_steps() - self.step
         st = _native.HeatRunStats()
-        _native.call("heat_solver_run", self._h, int(steps), ctypes.byref(st))
+        _native.call("heat_solver_run" if wait else "heat_solver_enqueue", self._h, int(steps),
+                     ctypes.byref(st))
         return RunResult(st.steps_done, st.total_steps, bool(st.converged), st.converged_at,
                          st.last_resid, st.seconds, st.passes, st.exchanges, st.checks,
                          self.config.nx * self.config.ny, st.t_exchange, st.t_compute,

@@ -167,3 +167,25 @@ def test_tb_edge_subboxes_bitwise(gpu, tmp_path, edge_frac):
                        capture_output=True, text=True, timeout=300, check=True)
         got[backend] = json.loads((d / "c.json").read_text())
     assert got["hip"]["hash"] == got["cpu"]["hash"]
+
+
+@pytest.mark.parametrize("kw", [dict(nx=300, ny=517), dict(nx=1024, ny=8192)])
+def test_enqueued_runs_match_synchronous(gpu, kw):
+    # run(wait=False) x 3 then run(0) (bench.py's timed loop) == one run of
+    # the same steps: state, step count; state access completes pending runs.
+    cfg = HeatConfig(steps=0, init="random", seed=21, backend="hip", **kw)
+    with HeatSolver(cfg) as a:
+        rs = [a.run(97, wait=False) for _ in range(3)]
+        assert all(r.steps_done == 97 for r in rs)
+        done = a.run(0)
+        assert done.steps_done == 0 and done.resident_giveups == 0
+        ga = a.gather()
+        a.run(50, wait=False)
+        gb = a.gather()  # completes the pending run first
+        step_b = a.step
+    with HeatSolver(cfg) as b:
+        b.run(291)
+        want = b.gather()
+        b.run(50)
+        want_b = b.gather()
+    assert np.array_equal(ga, want) and np.array_equal(gb, want_b) and step_b == 341
