@@ -11,7 +11,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -79,8 +82,29 @@ struct Options {
   bool json = false, dump_initial = false;
 };
 
+// The live solvers of a single-process multi-rank run (heat --gpus N): a
+// failing rank aborts its peers' solvers (Solver::abort: ncclCommAbort, or
+// the communicator abandoned while captured graphs hold it) so that their
+// waits on it end and every thread can be joined.  A rank removes its entry
+// under the lock before its solver is destroyed, so an abort never runs on a
+// solver being destroyed.
+struct RankRegistry {
+  std::mutex mu;
+  std::vector<Solver*> solvers;
+  void set(int r, Solver* s) {
+    std::lock_guard<std::mutex> lk(mu);
+    solvers[size_t(r)] = s;
+  }
+  void abort_peers(int r) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < solvers.size(); ++i)
+      if (int(i) != r && solvers[i]) solvers[i]->abort();
+  }
+};
+
 // One rank's whole run: banners, solver, output, reference-style lines.
-void run_rank(const Options& o, const Params& P, std::unique_ptr<Transport> tr) {
+void run_rank(const Options& o, const Params& P, std::unique_ptr<Transport> tr,
+              RankRegistry* reg = nullptr) {
   const int rank = tr->rank(), world = tr->world();
   const bool root = rank == 0;
 
@@ -97,6 +121,14 @@ void run_rank(const Options& o, const Params& P, std::unique_ptr<Transport> tr) 
   }
 
   Solver S(P, std::move(tr));
+  struct Registered {  // unregistered before S is destroyed (on any exit)
+    RankRegistry* reg;
+    int r;
+    ~Registered() {
+      if (reg) reg->set(r, nullptr);
+    }
+  } registered{reg, rank};
+  if (reg) reg->set(rank, &S);
   if (!o.resume.empty()) S.read_bin(o.resume);
 
   const bool small = P.nx * P.ny <= (int64_t(1) << 24);
@@ -384,6 +416,12 @@ int main(int argc, char** argv) {
       hub = loopback_hub_create(gpus);
     std::vector<std::thread> threads;
     std::vector<std::string> errors(gpus);
+    RankRegistry reg;
+    reg.solvers.assign(size_t(gpus), nullptr);
+    std::mutex done_mu;
+    std::condition_variable done_cv;
+    int done = 0;
+    bool failed = false;
     for (int r = 0; r < gpus; ++r)
       threads.emplace_back([&, r] {
         try {
@@ -393,28 +431,52 @@ int main(int argc, char** argv) {
           // initialises on its own thread, concurrently.
           run_rank(o, Pr,
                    rccl ? make_rccl_transport(r, gpus, uid, Pr.device)
-                        : make_loopback_transport(hub, r, Pr.device));
+                        : make_loopback_transport(hub, r, Pr.device),
+                   &reg);
         } catch (const std::exception& e) {
           errors[r] = e.what();
-          if (hub) {
-            // Loopback peers blocked on this rank's messages throw in turn.
-            loopback_hub_fail(hub);
-          } else {
-            // RCCL peers would block in ncclGroupEnd / collectives waiting
-            // for this rank: report and end the process now (a fresh failure
-            // exit; the driver reclaims the device queues).
-            std::fprintf(stderr, "heat: rank %d error: %s\n", r, e.what());
-            std::fflush(stderr);
-            std::_Exit(1);
+          {
+            std::lock_guard<std::mutex> lk(done_mu);
+            failed = true;
           }
+          // Loopback peers blocked on this rank's messages throw in turn;
+          // RCCL peers' solvers are aborted (their watched waits throw).
+          if (hub) loopback_hub_fail(hub);
+          else reg.abort_peers(r);
         }
+        std::lock_guard<std::mutex> lk(done_mu);
+        ++done;
+        done_cv.notify_all();
       });
+    {
+      // After a failure every peer gets HEAT_GROUP_ABORT_S (60 s) to unwind;
+      // a thread still stuck then (a wait that never polls) ends the process
+      // instead of hanging it.
+      std::unique_lock<std::mutex> lk(done_mu);
+      done_cv.wait(lk, [&] { return done == gpus || failed; });
+      if (done < gpus) {
+        const double grace = std::getenv("HEAT_GROUP_ABORT_S") ? std::atof(std::getenv("HEAT_GROUP_ABORT_S")) : 60.0;
+        if (!done_cv.wait_for(lk, std::chrono::duration<double>(grace), [&] { return done == gpus; })) {
+          for (int r = 0; r < gpus; ++r)
+            if (!errors[r].empty()) std::fprintf(stderr, "heat: rank %d error: %s\n", r, errors[r].c_str());
+          std::fprintf(stderr, "heat: %d of %d ranks did not unwind within %.0f s; exiting\n",
+                       gpus - done, gpus, grace);
+          std::fflush(stderr);
+          std::_Exit(1);
+        }
+      }
+    }
     for (auto& t : threads) t.join();
     if (hub) loopback_hub_destroy(hub);
     // Report the failing rank, not the peers it unblocked.
     int first = -1;
+    auto echo = [](const std::string& e) {
+      return e.find("a peer rank failed") != std::string::npos ||
+             e.find("run aborted") != std::string::npos ||
+             e.find("communicator was aborted") != std::string::npos;
+    };
     for (int r = 0; r < gpus && first < 0; ++r)
-      if (!errors[r].empty() && errors[r].find("a peer rank failed") == std::string::npos) first = r;
+      if (!errors[r].empty() && !echo(errors[r])) first = r;
     for (int r = 0; r < gpus && first < 0; ++r)
       if (!errors[r].empty()) first = r;
     if (first >= 0) {

@@ -152,9 +152,10 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     }
   };
 
-  // A check's wave max waiting for its atomic (RES 1).
+  // A check's wave max waiting for its atomic (RES 1); the next check.
   float pend_m = 0.f;
   int pend_c = -1;
+  int next_chk = 0;
   auto flush_resid = [&]() {
     if constexpr (RES == 1) {
       if (pend_c >= 0) {
@@ -181,11 +182,12 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
             nopub ? false : band_lane, vlane, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
-    // The check of this pass (at most one, at an even level), if any.
+    // The check of this pass (at most one, at an even level), if any: the
+    // checks come in pass order, so one kernel-argument load per pass (a scan
+    // of all of them was up to 64 dependent scalar loads per pass).
     int ci = -1;
     if constexpr (RES == 1) {
-      for (int c = 0; c < ra.nchk; ++c)
-        if (ra.chk_pass[c] == p) ci = c;
+      if (next_chk < ra.nchk && ra.chk_pass[next_chk] == p) ci = next_chk++;
     }
     int acc_step = ci >= 0 ? ra.chk_step[ci] - 1 : -1;  // its step index (odd: an up step)
     opaque32(acc_step);

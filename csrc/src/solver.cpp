@@ -1194,7 +1194,8 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   // cost the 1024 x 8192 plate 2 % at a check every 100 steps.
   const int64_t L = std::lcm<int64_t>(C, std::max(1, T_));
   const int64_t unit = L <= 1024 ? L : C;
-  const int64_t seg_cap = unit * std::max<int64_t>(1, (1024 + unit - 1) / unit);
+  const int64_t want = std::max(1, env_int("HEAT_SEG_STEPS", 1024));  // A/B knob
+  const int64_t seg_cap = unit * std::max<int64_t>(1, (want + unit - 1) / unit);
   auto* gate_h = static_cast<gpu::DeviceGate*>(h_gate_);
   HIP_CHECK(hipMemsetAsync(d_gate_, 0, sizeof(gpu::DeviceGate), s_comp_));
   HIP_CHECK(hipMemsetAsync(d_resid_, 0, 4, s_comp_));
