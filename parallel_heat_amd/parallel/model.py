@@ -22,6 +22,9 @@ multi-GPU number, and that the autotune uses to skip candidates it rules out:
 
 All parameters are stated in ``XGMI`` / ``RATE_POINTS`` and returned with
 every prediction, so a measured SCALE record can be read against them.
+``fit_exchange`` replaces XGMI's latency and bandwidth with values fitted to
+grouped exchanges timed on the real ranks (bench.py does this before it
+prunes autotune candidates; the measured points are in the JSON line).
 """
 from __future__ import annotations
 
@@ -49,12 +52,13 @@ XGMI = {
 # resident workgroup tiles, r4t6), profiles/r3_tile.md (2048 x 8192,
 # 4096 x 4096: level-split pipelines), BENCH (8192 x 8192).
 RATE_POINTS: List[tuple] = [
-    # (strip-rows per SIMD, Tcells/s)
+    # (strip-rows per SIMD, Tcells/s); round 5, enqueued bench steps
+    # (profiles/r5_raw/r5f_b*.txt, r5c_b1192.txt)
     (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
-    (36.0, 4.0),    # 1024 x 8192 3.99 / 2048 x 4096 4.08 (8 GPUs), resident tiles
-    (72.0, 3.75),   # 2048 x 8192 / 4096 x 4096 (4 GPUs), split pipelines
-    (144.0, 4.6),   # 4096 x 8192 (2 GPUs)
-    (288.0, 5.1),   # 8192 x 8192 (1 GPU)
+    (36.0, 4.0),    # 1024 x 8192 4.02 / 2048 x 4096 4.01 (8 GPUs), resident tiles
+    (72.0, 3.92),   # 2048 x 8192 3.92 / 4096 x 4096 3.92 (4 GPUs), split pipelines
+    (144.0, 4.9),   # 4096 x 8192 4.91 (2 GPUs)
+    (288.0, 5.1),   # 8192 x 8192 5.04-5.21 (1 GPU)
 ]
 
 SIMDS = 1024

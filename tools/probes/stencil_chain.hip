@@ -158,5 +158,10 @@ int main() {
   run<8, 1, 0>(cus, clk);
   run<8, 1, 1>(cus, clk);
   run<8, 1, 16>(cus, clk);
+  // One stage of the depth-12 level-split pipeline (6 levels per wave):
+  // DPP shifts, ds_bpermute shifts (the split kernel's), no shifts.
+  run<6, 1, 0>(cus, clk);
+  run<6, 1, 4>(cus, clk);
+  run<6, 1, 1>(cus, clk);
   return 0;
 }
