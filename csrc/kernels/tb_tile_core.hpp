@@ -304,16 +304,20 @@ struct Tile {
     }
   }
 
-  // acc without branches: `take` (uniform) and res_lane select the max.
+  // acc without branches: `take` (uniform), res_lane and the lane's element
+  // count fold into one select per element (the uniform row bit ANDs into the
+  // per-lane masks on the scalar unit), then two NaN-propagating
+  // v_maximum3_f32 with abs modifiers: 10 VALU per row (was 14: a select per
+  // element, then one for the lane and one for the row).
   __device__ __forceinline__ void acc_sel(const vecf& nw, const vecf& old, bool res_lane, int rc,
                                           bool take) {
-    float d[4];
+    float c[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = (j == 0 || rc > j) ? __builtin_fabsf(nw[j] - old[j]) : 0.f;
-    const float dm = __builtin_elementwise_maximum(__builtin_elementwise_maximum(d[0], d[1]),
-                                                   __builtin_elementwise_maximum(d[2], d[3]));
-    const float mm = __builtin_elementwise_maximum(m, res_lane ? dm : 0.f);
-    m = take ? mm : m;
+    for (int j = 0; j < 4; ++j) c[j] = (take && res_lane && (j == 0 || rc > j)) ? nw[j] - old[j] : 0.f;
+    m = __builtin_elementwise_maximum(
+        __builtin_elementwise_maximum(m, __builtin_fabsf(c[0])), __builtin_fabsf(c[1]));
+    m = __builtin_elementwise_maximum(
+        __builtin_elementwise_maximum(m, __builtin_fabsf(c[2])), __builtin_fabsf(c[3]));
   }
   __device__ __forceinline__ void acc(const vecf& nw, const vecf& old, bool res_lane, int rc) {
     // NaN-propagating max (v_maximum3_f32): a NaN or inf reaches the judge.
