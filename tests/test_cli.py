@@ -227,7 +227,7 @@ def test_cli_reference_lines_match(tmp_path, args):
         p = subprocess.run(cmd + ["--backend", "cpu"] + args, cwd=d, capture_output=True,
                            text=True, timeout=300, check=True,
                            env=dict(os.environ, PYTHONPATH=ROOT))
-        lines = [re.sub(r"[0-9.]+ (m?secs)", r"T \1", l) if l.startswith("Elapsed time") else l
+        lines = [re.sub(r"[0-9.]+ m?secs", "T (m)secs", l) if l.startswith("Elapsed time") else l
                  for l in p.stdout.splitlines()]
         files = {f.name: f.read_bytes() for f in sorted(d.iterdir())}
         outs[name] = (lines, files)
