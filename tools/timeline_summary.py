@@ -43,12 +43,12 @@ def load(dirpath):
     ranks = collections.defaultdict(lambda: {"kernels": [], "markers": []})
     for f in glob.glob(os.path.join(dirpath, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            pid = int(r.get("Process_Id") or r.get("Pid") or re.findall(r"(\d+)", f)[-1])
+            pid = int(r.get("Process_Id") or r.get("Pid") or re.findall(r"(\d+)", os.path.basename(f))[-1])
             ranks[pid]["kernels"].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                                           r["Kernel_Name"]))
     for f in glob.glob(os.path.join(dirpath, "**", "*marker_api_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            pid = int(r.get("Process_Id") or r.get("Pid") or 0)
+            pid = int(r.get("Process_Id") or r.get("Pid") or re.findall(r"(\d+)", os.path.basename(f))[-1])
             name = r.get("Function") or r.get("Operation") or r.get("Name") or ""
             ranks[pid]["markers"].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     return ranks
