@@ -167,6 +167,7 @@ class Solver {
   // kernel (even depths): remainder passes are then split into even parts.
   bool tile_sized() const;
   bool tile_sized_at(int depth) const;
+  bool resident_sized() const;
   // Passes for steps [step0, step0+n), cut at every check point (the
   // residual is the last level of its pass).
   std::vector<PassPlan> plan_passes(int64_t step0, int64_t n) const;

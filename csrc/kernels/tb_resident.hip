@@ -111,7 +111,7 @@ ResPlan plan_res(const Box& box, int depth, int xl, const TbTuning& tune) {
   struct Shape {
     int rows, waves;
   };
-  static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {12, 16}};
+  static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {12, 16}, {20, 16}};
   for (const Shape& sh : kShapes) {
     if (tune.tile_rows > 0 && sh.rows != tune.tile_rows) continue;
     if (tune.tile_waves > 0 && sh.waves != tune.tile_waves) continue;

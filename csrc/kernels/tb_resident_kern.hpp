@@ -37,8 +37,6 @@ struct ResArgs {
                         // publish, 3 every tile on the masked path
 };
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
 // Neighbour waits give up after this many polls (~0.3 s with s_sleep 2).
 constexpr unsigned kSpinLimit = 1u << 22;
 
@@ -136,19 +134,19 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
   const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
   TileXc<NW> xc{xch, w, lane, 1, 0, 0, vecf{}};
 
-  // The publish sink of a pass's last step: edge bands into xb[p & 1].
+  // The sinks of a pass's last step: edge bands into xb[p & 1] (Pub), the
+  // last pass's useful rows into dst (RowStoreSink).  Both branch-free (see
+  // RowStoreSink): with a per-row `if`, tiles of 36-40 rows per wave spilled
+  // 660-1000 B/lane, and 20 x 16 tiles 96 B.
   struct Pub {
     __amdgpu_buffer_rsrc_t rs;
     unsigned usemask, bandmask;
-    bool store_lane, band_lane;
-    int vlane, xrow0, xpitch;
+    int vs, vb;  // voffset of a core row's / a band row's store (kNoStore: none)
+    int xrow0, xpitch;
     __device__ __forceinline__ void row(int r, const vecf& v, const vecf&) {
-      if ((usemask >> r) & 1u) {
-        const bool st = ((bandmask >> r) & 1u) ? store_lane : band_lane;
-        if (st)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, vlane,
-                                                 xrow0 + r * xpitch, 16);
-      }
+      const int vo = ((usemask >> r) & 1u) ? (((bandmask >> r) & 1u) ? vs : vb) : kNoStore;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, vo, xrow0 + r * xpitch,
+                                             16);
     }
   };
 
@@ -178,10 +176,15 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     opaque32(xr0);
     opaque32(xp);
     const bool nopub = ra.diag & 4;
-    Pub pub{xr[p & 1], usemask, nopub ? 0u : bandmask, nopub ? false : store_lane,
-            nopub ? false : band_lane, vlane, xr0, xp};
+    // Masks opaque per pass: hoisted out of the pass loop, the per-row
+    // voffset selects became R loop-invariant VGPRs (and spilled).
+    unsigned pum = nopub ? 0u : usemask, pbm = bandmask;
+    opaque(pum);
+    opaque(pbm);
+    Pub pub{xr[p & 1], pum, pbm, store_lane ? vlane : kNoStore, band_lane ? vlane : kNoStore, xr0, xp};
     int64_t off0 = row0 * pitch;  // this wave's first row in dst (the last pass stores)
     opaque(off0);
+    RowStoreSink fin{dst + off0, pitch, pum, store_lane ? vlane : kNoStore};
     // The check of this pass (at most one, at an even level), if any: the
     // checks come in pass order, so one kernel-argument load per pass (a scan
     // of all of them was up to 64 dependent scalar loads per pass).
@@ -193,7 +196,7 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
     opaque32(acc_step);
     unsigned rm = ci >= 0 ? resmask : 0u;  // the check step's residual rows
     opaque(rm);
-    tile_pass_steps<RES == 1 ? 3 : 0, LAST ? 1 : 3>(
+    tile_pass_steps<RES == 1 ? 3 : 0, 3>(
         K,
         [&](auto down_c, auto what_c, auto acc_c, int s) {
           constexpr bool D = decltype(down_c)::value;
@@ -205,9 +208,14 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
           // The last step always runs the accumulating body: rows only if
           // the check is there.
           const unsigned rms = s == acc_step ? rm : 0u;
-          T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-              first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub,
-              rms, res_rc);
+          if constexpr (LAST)
+            T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
+                first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &fin,
+                rms, res_rc);
+          else
+            T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
+                first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub,
+                rms, res_rc);
         },
         acc_step);
     if constexpr (RES == 1) {
@@ -352,8 +360,10 @@ int occ_res() {
 
 // Instantiated shapes (rows per wave, waves per workgroup): the tile
 // planner's set up to 24 rows per wave (the resident grid must be one
-// dispatch round, so only blocks with few tiles qualify).
-#define HEAT_RES_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(12, 16)
+// dispatch round, so only blocks with few tiles qualify), and 20 x 16: 320
+// rows per tile, one tile per CU at 4 waves per SIMD, the 4-GPU per-rank
+// blocks (2048 x 8192: 36 strips x 7 chunks; 4096 x 4096: 18 x 14).
+#define HEAT_RES_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(12, 16) X(20, 16)
 
 template <int R, int NW, int XL>
 void launch_res_x(const ResArgs& ra, int blocks, hipStream_t st) {

@@ -107,7 +107,7 @@ void step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, 
   struct Shape {
     int rows, waves;
   };
-  static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}};
+  static constexpr Shape kShapes[] = {{12, 8}, {13, 8}, {14, 8}, {16, 8}, {20, 8}, {24, 8}, {28, 8}, {32, 8}, {12, 16}, {20, 16}};
   // Lane shifts: mixed (2: the left shift a DPP wave shift folded into the
   // add, the right one ds_bpermute issued ahead; +3-6 % over ds_bpermute for
   // both, which waited on LDS issue 13 % of the time, profiles/r3_tile.md)

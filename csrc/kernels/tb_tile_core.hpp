@@ -12,6 +12,7 @@ namespace heat::gpu::tbw {
 using tbdetail::TbArgs;
 using tbdetail::TbBox;
 typedef float vecf __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef HEAT_TILE_PD
 #define HEAT_TILE_PD 3  // rows the ds_bpermute lane shifts run ahead
@@ -340,6 +341,26 @@ constexpr int tile_waves_per_simd() {
 
 struct TileNoSink {
   __device__ __forceinline__ void row(int, const vecf&, const vecf&) {}
+};
+
+// The last step's stores of a wave's useful rows to dst, branch-free: one
+// buffer resource per row (the strip's 256 columns, built on the scalar
+// unit: no 32-bit limit on the field's size) and an out-of-range voffset
+// for a lane or row that does not store (the range check drops it).  A
+// per-row `if` around a store made every row of the step its own basic
+// block; the step's lane shifts were then hoisted ahead of its barrier and
+// tall tiles spilled (profiles/r5_spills.md).
+constexpr int kNoStore = int(0x80000000u);
+struct RowStoreSink {
+  float* base;  // the wave's first row, the strip's first column
+  int64_t pitch;
+  unsigned usemask;
+  int vs;  // this lane's voffset (kNoStore: not a stored lane)
+  __device__ __forceinline__ void row(int r, const vecf& v, const vecf&) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + r * pitch, 0, 1024, 0x00020000);
+    const int vo = ((usemask >> r) & 1u) ? vs : kNoStore;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, vo, 0, 0);
+  }
 };
 
 // Neighbour rows through LDS, one workgroup barrier per step placed HALFWAY

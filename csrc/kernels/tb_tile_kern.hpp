@@ -76,7 +76,10 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
   // RES 1: the residual of step res_level - 1: a uniform row mask, zero in
   // every other step (tile_pass_steps ACC_MODE 1).
   const int rs = RES ? a.res_level - 1 : -1;
-  tile_pass_steps<RES == 1 ? 1 : 0, 1>(K, [&](auto down_c, auto what_c, auto acc_c, int s) {
+  unsigned sm = usemask;
+  opaque(sm);
+  RowStoreSink fin{dst + off0, pitch, sm, store_lane ? 16 * lane : kNoStore};
+  tile_pass_steps<RES == 1 ? 1 : 0, 3>(K, [&](auto down_c, auto what_c, auto acc_c, int s) {
     constexpr bool D = decltype(down_c)::value;
     xc.p = s & 1;
     // Down: the last row needs the wave below; so does the next (up) step's first.
@@ -87,8 +90,7 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
     unsigned rm = s == rs ? ~0u : 0u;
     opaque(rm);
     T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-        first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch,
-        static_cast<TileNoSink*>(nullptr), rm);
+        first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &fin, rm);
   });
   return T.m;
 }
@@ -174,7 +176,7 @@ int occ_r() {
 }
 
 // Instantiated (rows per wave, waves per workgroup).
-#define HEAT_TILE_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16)
+#define HEAT_TILE_SHAPES(X) X(12, 8) X(13, 8) X(14, 8) X(16, 8) X(20, 8) X(24, 8) X(28, 8) X(32, 8) X(12, 16) X(20, 16)
 
 // The entry points of one lane-shift build (tb_tile_xl<XL>.hip).
 template <int XL>

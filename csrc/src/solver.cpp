@@ -133,7 +133,11 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   const int local_world = std::min(world, std::max(1, env_int("LOCAL_WORLD_SIZE", world)));
   const int res_env = env_int("HEAT_TB_RESIDENT", 1);
   resident_force_ = res_env == 2;
-  resident_ = tile_sized() && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
+  // Blocks past the tile threshold whose resident grid still fits one
+  // dispatch round (the 4-GPU blocks 2048 x 8192 / 4096 x 4096: 20 x 16
+  // tiles) go resident too; other large blocks never allocate the exchange
+  // fields (two more fields' worth of memory).
+  resident_ = (tile_sized() || resident_sized()) && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
               !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
               (world == 1 || ndev >= local_world || resident_force_);
   if (const char* e = std::getenv("HEAT_TB_RES_GIVEUP"); e && std::strcmp(e, "defer") == 0)
@@ -350,6 +354,17 @@ int Solver::auto_tb_depth() const {
 }
 
 bool Solver::tile_sized() const { return tile_sized_at(T_); }
+
+bool Solver::resident_sized() const {
+  // Every rank's owned block has a one-round resident plan at depth T_
+  // (spans over deep-halo boxes are checked again, resident_span).
+  if (!on_gpu() || !tb_kernel() || T_ < 4 || T_ % 2 != 0) return false;
+  for (int r = 0; r < cart_.world; ++r) {
+    const Block b = make_block(cart_, r, P_.nx, P_.ny);
+    if (!gpu::tb_resident_fits(Box{0, b.lx, 0, b.ly}, T_)) return false;
+  }
+  return true;
+}
 
 bool Solver::tile_sized_at(int depth) const {
   // The same rule as gpu::tb_auto_variant (strip-rows per SIMD of the owned

@@ -26,6 +26,8 @@ def _solve(cfg, steps, resident, monkeypatch, chunks=None):
 @pytest.mark.parametrize("nx,ny,steps,fits", [
     (1024, 8192, 100, True),    # the 8-GPU 1-D per-rank block as a plate
     (2048, 4096, 60, True),     # the 8-GPU 2-D (4 x 2) per-rank block
+    (2048, 8192, 60, True),     # the 4-GPU 1-D per-rank block: 20 x 16 tiles (36 x 7)
+    (4096, 4096, 60, True),     # the 4-GPU 2-D (2 x 2) per-rank block: 20 x 16 (18 x 14)
     (203, 517, 97, True),       # partial strips and tiles, a short remainder
     (300, 1000, 50, True),
     (40, 70, 36, True),         # fewer rows than one tile
@@ -81,6 +83,47 @@ def test_resident_multirank_deep_halo(gpu, monkeypatch, world, kw):
     assert np.array_equal(got, want), np.abs(got - want).max()
 
 
+@pytest.fixture
+def res_shape():
+    """Force the resident planner's tile shape (rows per wave, waves)."""
+    from parallel_heat_amd import ops
+    saved = ops.tb_tuning()
+
+    def set_(rows, waves):
+        t = ops.tb_tuning()
+        t.tile_rows, t.tile_waves = rows, waves
+        ops.set_tb_tuning(t)
+    yield set_
+    ops.set_tb_tuning(saved)
+
+
+@pytest.mark.parametrize("world,kw", [
+    (1, dict(nx=203, ny=517)),                       # every Dirichlet edge, partial strips
+    (1, dict(nx=700, ny=300)),                       # tiles taller than the plate's chunks
+    (2, dict(nx=1024, ny=1024, decomp="rows")),      # deep halos through 20 x 16 tiles
+    (4, dict(nx=1024, ny=1024, px=2, py=2)),         # 2-D: ghost columns and corners
+])
+def test_resident_20x16_tiles(gpu, monkeypatch, res_shape, world, kw):
+    # The 4-GPU shape (320-row tiles, 16 waves of 20 rows) forced on small
+    # blocks, so its edge, remainder and multi-rank paths run on one GPU.
+    res_shape(20, 16)
+    cfg = HeatConfig(steps=0, init="random", seed=9, backend="hip", **kw)
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "2" if world > 1 else "1")
+    if world == 1:
+        with HeatSolver(cfg) as s:
+            r = s.run(200)
+            got = s.gather()
+        res = [r]
+    else:
+        out = run_group(cfg, world, lambda s: (s.run(200), s.gather()))
+        res = [o[0] for o in out]
+        got = next(g for _, g in out if g is not None)
+    assert all(r.resident_passes > 0 for r in res), res
+    single = cfg.replace(decomp="auto", px=0, py=0, backend="cpu", tb_depth=1)
+    want, _ = _solve(single, 200, False, monkeypatch)
+    assert np.array_equal(got, want), np.abs(got - want).max()
+
+
 @pytest.mark.parametrize("interval", [50, 20, 7])
 def test_resident_with_checks(gpu, monkeypatch, interval):
     # Checks at even levels ride inside resident spans (every 20 / 50 steps
@@ -105,6 +148,7 @@ def test_resident_with_checks(gpu, monkeypatch, interval):
     (1, dict(nx=1024, ny=8192), 20, 3),               # step 60 ends pass 5
     (1, dict(nx=1024, ny=8192), 50, 2),               # step 100, level 4 of pass 9
     (1, dict(nx=1024, ny=8192), 50, 5),               # step 250, level 10 of pass 21
+    (1, dict(nx=2048, ny=8192), 20, 4),               # 20 x 16 tiles (RES 1 build)
     (2, dict(nx=1024, ny=1024, decomp="rows"), 20, 4),  # deep halos: the owned rows only
     (4, dict(nx=1024, ny=1024, px=2, py=2), 50, 1),     # 2-D blocks: owned rows and columns only
 ])
