@@ -210,15 +210,20 @@ __device__ __forceinline__ void resident_run(const ResArgs& ra, const TbBox& bx,
           const unsigned rms = s == acc_step ? rm : 0u;
           if constexpr (LAST)
             T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-                first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &fin,
+                first_nb, xc, up, rowmask, usemask, store_lane, rc, &fin,
                 rms, res_rc);
           else
             T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-                first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &pub,
+                first_nb, xc, up, rowmask, usemask, store_lane, rc, &pub,
                 rms, res_rc);
         },
         acc_step);
     if constexpr (RES == 1) {
+      // Pin the residual here: consumed only under `ci >= 0`, its max chain
+      // was sunk into that branch, which kept every row's old value of the
+      // pass's last step alive until then (20 x 16: 352 -> 108 B/lane of
+      // scratch, 12 x 16: 48 -> 0).
+      asm volatile("" : "+v"(T.m));
       if (ci >= 0) {
         // Deferred: the atomic goes out after the next pass's ghost loads
         // (refill), not in front of the publish's vmcnt(0) drain, where ~63

@@ -240,15 +240,13 @@ struct Tile {
   // lets the register allocator put new row r where old row r -/+ 1 was (dead
   // by then) and be back at the loop's assignment after two steps: one
   // direction only needed a copy of every row per step at the back-edge.
-  // WHAT 1 (LAST): the launch's last step stores every useful row as soon as
-  // it is computed (dst + off0 + r * pitch, this lane's columns if
-  // store_lane); WHAT 3: every row goes to sink->row(r, new, old) (the
-  // resident kernel's edge-band publish, tb_resident.hip).  ACC: this step
-  // accumulates max |new - old| over the useful rows in resmask.
+  // WHAT 3: every row goes to sink->row(r, new, old) as soon as it is
+  // computed (the last step's stores: RowStoreSink, or the resident
+  // kernel's edge-band publish); 0: nothing.  ACC: this step accumulates
+  // max |new - old| over the useful rows in resmask.
   template <bool DOWN, int WHAT, bool ACC = false, class Xc, class Sink = TileNoSink>
   __device__ __forceinline__ void step(const vecf& first_nb, Xc& xc, const Upd<MODE, XL>& up,
                                        unsigned rowmask, unsigned usemask, bool store_lane, int rc,
-                                       float* __restrict__ dst, int64_t off0, int64_t pitch,
                                        Sink* sink = nullptr, unsigned resmask = ~0u,
                                        int res_rc = -1) {
     // Residual window (the resident kernel's deep-halo boxes: the owned block
@@ -287,13 +285,7 @@ struct Tile {
       u[r] = up.apply(n, cur, so, wl[r], er[r], (rowmask >> r) & 1u);
       if (i == 0) xc.publish(0, u[r]);
       if (i == R - 1) xc.publish(1, u[r]);
-      if constexpr (WHAT == 1) {
-        if ((usemask >> r) & 1u) {
-          if (store_lane) *reinterpret_cast<vecf*>(dst + off0 + r * pitch) = u[r];
-        }
-      } else if constexpr (WHAT == 3) {
-        sink->row(r, u[r], cur);
-      }
+      if constexpr (WHAT == 3) sink->row(r, u[r], cur);
       if constexpr (ACC) {
         // Branch-free: a uniform branch per row split the step into basic
         // blocks the scheduler cannot interleave.

@@ -90,7 +90,7 @@ __device__ __forceinline__ float tile_run(const TbArgs& a, const TbBox& bx, int 
     unsigned rm = s == rs ? ~0u : 0u;
     opaque(rm);
     T.template step<D, decltype(what_c)::value, decltype(acc_c)::value>(
-        first_nb, xc, up, rowmask, usemask, store_lane, rc, dst + lo, off0, pitch, &fin, rm);
+        first_nb, xc, up, rowmask, usemask, store_lane, rc, &fin, rm);
   });
   return T.m;
 }

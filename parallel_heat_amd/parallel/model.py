@@ -13,14 +13,15 @@ multi-GPU number, and that the autotune uses to skip candidates it rules out:
   rates are this build's measured whole-solver ``bench.py`` plates whose top
   and bottom rows are plate edges (the slowest rank of a decomposition,
   which the max over ranks reports), interpolated in strip-rows per SIMD --
-  the planner's own measure of the work per launch (RATE_POINTS).
+  the planner's own measure of the work per launch (RESIDENT_POINTS when
+  the span's box has a one-round resident plan, STREAM_POINTS otherwise).
 * exchange: one grouped RCCL send/recv phase per m*K steps (deep halos),
   every message on its own xGMI link (full mesh, one hop): a fixed latency
   plus the largest message over the link bandwidth (XGMI).  2-D grids add
   the pack / unpack launches of the E/W columns and ghost corners.
 * all-reduce: one 4-byte ncclAllReduce(max) per convergence check.
 
-All parameters are stated in ``XGMI`` / ``RATE_POINTS`` and returned with
+All parameters are stated in ``XGMI`` / ``*_POINTS`` and returned with
 every prediction, so a measured SCALE record can be read against them.
 ``fit_exchange`` replaces XGMI's latency and bandwidth with values fitted to
 grouped exchanges timed on the real ranks (bench.py does this before it
@@ -47,34 +48,63 @@ XGMI = {
 
 # Whole-solver rate (Tcells/s of owned cells) of one MI355X on a bench plate
 # (plate edges top and bottom) vs strip-rows per SIMD of that plate (232
-# useful columns per 256-column strip at depth 12, 1024 SIMDs).  Measured
-# with this build: profiles/r4_resident.md (1024 x 8192 and 2048 x 4096:
-# resident workgroup tiles, r4t6), profiles/r3_tile.md (2048 x 8192,
-# 4096 x 4096: level-split pipelines), BENCH (8192 x 8192).
-RATE_POINTS: List[tuple] = [
-    # (strip-rows per SIMD, Tcells/s); round 5, enqueued bench steps
-    # (profiles/r5_raw/r5f_b*.txt, r5c_b1192.txt)
+# useful columns per 256-column strip at depth 12, 1024 SIMDs), in two
+# families: spans whose box has a one-dispatch-round resident plan (every
+# tile co-resident for all passes between exchanges, tb_resident.hip) and
+# the rest (level-split pipelines / per-pass tiles).  Round 5 measurements,
+# enqueued bench steps (profiles/r5_raw/r5h_*.txt, r5f_b*.txt, r5c_b1192.txt).
+RESIDENT_POINTS: List[tuple] = [
     (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
-    (36.0, 4.0),    # 1024 x 8192 4.02 / 2048 x 4096 4.01 (8 GPUs), resident tiles
-    (72.0, 3.92),   # 2048 x 8192 3.92 / 4096 x 4096 3.92 (4 GPUs), split pipelines
-    (144.0, 4.9),   # 4096 x 8192 4.91 (2 GPUs)
-    (288.0, 5.1),   # 8192 x 8192 5.04-5.21 (1 GPU)
+    (36.0, 4.03),   # 1024 x 8192 3.96 / 2048 x 4096 4.10 (8 GPUs): 12 x 16 tiles
+    (42.0, 4.29),   # 1192 x 8192 (the 1-D 8-GPU middle rank's first box): 14 x 8
+    (72.0, 5.29),   # 2048 x 8192 5.25-5.34 / 4096 x 4096 5.22-5.34 (4 GPUs): 20 x 16
 ]
+STREAM_POINTS: List[tuple] = [
+    (18.0, 3.0),    # extrapolated, unmeasured
+    (36.0, 3.3),    # 1024 x 8192 per-pass tiles (round 3/4: 3.23)
+    (72.0, 3.90),   # 2048 x 8192 3.90 / 4096 x 4096 3.90, split pipelines
+    (144.0, 4.9),   # 4096 x 8192 4.91 (2 GPUs)
+    (288.0, 5.05),  # 8192 x 8192 5.03-5.21 (1 GPU)
+]
+RATE_POINTS = STREAM_POINTS  # the large-block end (1 GPU) is a stream plate
 
 SIMDS = 1024
 STRIP_COLS = 232  # useful columns per 256-column strip at depth 12
+CUS = 256
+
+# The resident planner's shapes (rows per wave, waves, workgroups per CU at
+# their VGPR budget): csrc/kernels/tb_resident.hip plan_res.
+RES_SHAPES = [(12, 8, 2), (13, 8, 2), (14, 8, 2), (16, 8, 2), (20, 8, 1), (24, 8, 1),
+              (12, 16, 1), (20, 16, 1)]
 
 
-def rate_tcells(rows: int, cols: int) -> float:
-    """Interpolated whole-solver rate of a rows x cols block (Tcells/s)."""
-    srps = math.ceil(cols / STRIP_COLS) * rows / SIMDS
-    pts = RATE_POINTS
+def resident_fits(rows: int, cols: int, depth: int = 12) -> bool:
+    """A rows x cols box has a one-round resident plan (all tiles co-resident)."""
+    strips = math.ceil(cols / STRIP_COLS)
+    for r, nw, occ in RES_SHAPES:
+        h = r * nw - 2 * depth
+        if h >= depth and strips * math.ceil(rows / h) <= CUS * occ:
+            return True
+    return False
+
+
+def _interp(pts, srps: float) -> float:
     if srps <= pts[0][0]:
         return pts[0][1] * srps / pts[0][0] if srps > 0 else pts[0][1]
     for (x0, y0), (x1, y1) in zip(pts, pts[1:]):
         if srps <= x1:
             return y0 + (y1 - y0) * (srps - x0) / (x1 - x0)
     return pts[-1][1]
+
+
+def rate_tcells(rows: int, cols: int, resident: bool = None) -> float:
+    """Interpolated whole-solver rate of a rows x cols block (Tcells/s);
+    `resident` (default: whether the block itself fits one round) picks the
+    family."""
+    srps = math.ceil(cols / STRIP_COLS) * rows / SIMDS
+    if resident is None:
+        resident = resident_fits(rows, cols)
+    return _interp(RESIDENT_POINTS if resident else STREAM_POINTS, srps)
 
 
 def _grid(cfg: HeatConfig, world: int) -> tuple:
@@ -130,12 +160,13 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
     if world > 1 and schedule != "sync":
         m = 1
     H = m * depth
-    # Deep-halo ghost rows recomputed on the decomposed axes (both sides of an
-    # inner rank): the first pass's box (resident launches keep it for all m
-    # passes).
-    ext_r = 2 * (H - depth) if px > 1 else 0
-    ext_c = 2 * (H - depth) if py > 1 else 0
-    rate = rate_tcells(lx, ly) * 1e12
+    # Deep-halo ghost rows recomputed on the decomposed axes: the first
+    # pass's box (resident launches keep it for all m passes) grows by H - K
+    # per neighbour side, two for an inner rank (p > 2), one with p = 2.
+    ext_r = (2 if px > 2 else 1) * (H - depth) if px > 1 else 0
+    ext_c = (2 if py > 2 else 1) * (H - depth) if py > 1 else 0
+    resident = schedule == "sync" and resident_fits(lx + ext_r, ly + ext_c, depth)
+    rate = rate_tcells(lx, ly, resident) * 1e12
     cells = (lx + ext_r) * (ly + ext_c)
     compute_s = cells * 1000 / rate
     exchanges = math.ceil(1000 / H) if world > 1 else 0
@@ -151,7 +182,7 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
         # launches and every pass pays a cross-stream join (~10-15 us each,
         # profiles/overlap_probe_r1.md); no resident spans (split kernels).
         passes = math.ceil(1000 / depth)
-        per_pass = lx * ly * depth / (rate_tcells(lx, ly) * 1e12 * 0.8)
+        per_pass = lx * ly * depth / (rate_tcells(lx, ly, False) * 1e12 * 0.8)
         compute_s = passes * (max(per_pass, t_ex) + 25e-6)
         ex_total = 0.0
     checks = math.floor(1000 / cfg.check_interval) if cfg.converge else 0
@@ -165,7 +196,8 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
         "reduce_ms": round(reduce_s * 1e3, 4),
         "ms_per_1000": round(total * 1e3, 4),
         "tcells_per_s": round(cfg.nx * cfg.ny * 1000 / total / 1e12, 3),
-        "rank_rate_tcells": round(rate_tcells(lx, ly), 3),
+        "rank_rate_tcells": round(rate / 1e12, 3),
+        "resident": bool(resident) if schedule == "sync" else False,
         "message_bytes": msg,
     }
 
@@ -182,5 +214,6 @@ def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3,
 
 
 def model_params(xgmi: Dict = None) -> Dict:
-    return {"xgmi": dict(xgmi or XGMI), "rate_points": [list(p) for p in RATE_POINTS],
+    return {"xgmi": dict(xgmi or XGMI), "resident_points": [list(p) for p in RESIDENT_POINTS],
+            "stream_points": [list(p) for p in STREAM_POINTS],
             "strip_cols": STRIP_COLS, "simds": SIMDS}

@@ -56,9 +56,25 @@ def test_model_single_gpu_is_the_plate_rate():
 
 def test_model_more_ranks_never_slower_per_rank_block():
     from parallel_heat_amd.parallel.model import rate_tcells
-    # Rates are monotone-ish in work per SIMD within the measured range.
-    assert rate_tcells(8192, 8192) >= rate_tcells(4096, 8192) >= rate_tcells(2048, 8192)
-    assert rate_tcells(512, 8192) < rate_tcells(1024, 8192)
+    # Within a family, rates are monotone in work per SIMD over the measured range.
+    assert (rate_tcells(8192, 8192, False) >= rate_tcells(4096, 8192, False)
+            >= rate_tcells(2048, 8192, False) >= rate_tcells(1024, 8192, False))
+    assert rate_tcells(2048, 8192, True) >= rate_tcells(1024, 8192, True) > rate_tcells(512, 8192, True)
+
+
+def test_model_resident_fits_mirrors_the_planner():
+    from parallel_heat_amd.parallel.model import predict, resident_fits
+    assert resident_fits(1024, 8192) and resident_fits(2048, 4096)        # 12 x 16: 252 / 234 tiles
+    assert resident_fits(1192, 8192)                                      # 14 x 8, two per CU
+    assert resident_fits(2048, 8192) and resident_fits(4096, 4096)        # 20 x 16: 252 tiles
+    assert resident_fits(4096 + 36, 4096 + 36)                            # 2 x 2, m = 4 box
+    assert not resident_fits(2048 + 2 * 84, 8192)                         # 1-D middle rank, m = 8
+    assert not resident_fits(8192, 8192) and not resident_fits(4096, 8192)
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    two_by_two = predict(cfg.replace(px=2, py=2, halo_passes=4), 4)
+    slabs = predict(cfg.replace(decomp="rows", halo_passes=8), 4)
+    assert two_by_two["resident"] and not slabs["resident"]
+    assert two_by_two["ms_per_1000"] < slabs["ms_per_1000"]
 
 
 class _FakeSolver:
