@@ -32,6 +32,12 @@
 #if HEAT_TB_PACKED && HEAT_TB_V != 4
 #error "the packed row update is written for float4 lanes"
 #endif
+// Main-loop stores as buffer stores: the row's buffer resource built on the
+// scalar unit (no 64-bit VALU address per row), a store-less lane given an
+// out-of-range voffset (no exec-mask branch per row).
+#ifndef HEAT_TB_BUFSTORE
+#define HEAT_TB_BUFSTORE 0
+#endif
 
 namespace heat::gpu::HEAT_TB_NS {
 
@@ -206,6 +212,7 @@ struct TbStream {
   // and the row arithmetic stays on the scalar unit.
   int lo = 0;
   bool nostore = false;  // diagnostics only (kTbDiagNoStore): timing without the stores
+  int vso = 0;  // HEAT_TB_BUFSTORE: this lane's store voffset (out of range: no store)
   bool cached_rows = false;  // diagnostics only (kTbDiagCachedRows): loads hit 4 rows
 
   // Level-split pipeline state (ROLE 1/2): a ring of kSplitRing rows of the
@@ -275,6 +282,26 @@ struct TbStream {
       off = *woff;
       *woff += pitch;
     }
+#if HEAT_TB_BUFSTORE
+    if constexpr (FAST) {
+      typedef unsigned uvec __attribute__((ext_vector_type(V)));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + off, 0, 4 * V * 64, 0x00020000);
+#if HEAT_TB_V == 4
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec, out), rs, vso, 0, 0);
+#else
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec, out), rs, vso, 0, 0);
+#endif
+      if constexpr (LASTRES) {
+        float d[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) d[j] = (store_lane && (j == 0 || rc > j)) ? __builtin_fabsf(out[j] - b[j]) : 0.f;
+#pragma unroll
+        for (int j = 0; j < V; j += 2)
+          m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(d[j], d[j + 1]));
+      }
+      return;
+    }
+#endif
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
       if constexpr (LASTRES) {
@@ -650,6 +677,7 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.qrb = int(rb);
       st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
+      st.vso = store_lane && !st.nostore ? 4 * V * lane : int(0x80000000u);
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
@@ -679,6 +707,7 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.qrb = int(rb);
       st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
+      st.vso = store_lane && !st.nostore ? 4 * V * lane : int(0x80000000u);
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     }

@@ -17,9 +17,13 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef HEAT_TILE_PD
 #define HEAT_TILE_PD 3  // rows the ds_bpermute lane shifts run ahead
 #endif
-#ifndef HEAT_TILE_PK
-#define HEAT_TILE_PK 0  // packed f32 update (Upd::apply)
-#endif
+// Waves of at most this many rows take the packed row update (Upd::apply
+// PK): on 12-row waves it measured +3-6 % (1024 x 8192 4.06-4.18 vs
+// 3.91-3.95, 2048 x 4096 4.17 vs 4.04, session r5j); its pair temporaries
+// spilled taller waves (20 x 16: 676 B/lane, 1.04 Tcells/s) and, next to
+// the residual code, the 12-row RES 1 builds (resident: 48 -> 200 B/lane),
+// which keep the scalar update.
+constexpr int kTilePkRows = 12;
 
 // Lane l <- lane l-1 / l+1.  Lanes 0 and 63 lie in the strip overlap
 // (don't-care values).  XL: 0 both shifts DPP wave shifts (folded into the
@@ -101,16 +105,16 @@ struct Upd {
   bool cm[4];
   // wl / er: the west neighbour of element 0 (lane l-1's element 3) and the
   // east neighbour of element 3 (lane l+1's element 0).
+  template <bool PK = false>
   __device__ __forceinline__ vecf apply(const vecf& a, const vecf& b, const vecf& c, float wl,
                                         float er, bool row_ok) const {
     vecf r;
-#if HEAT_TILE_PK
-    // Packed f32 (v_pk_add_f32 / v_pk_fma_f32) on the element pairs 0-1 and
-    // 2-3: the same per-element operations in the same order as stencil()
-    // (bitwise equal), ~14.5 VALU per row instead of 24-25; the horizontal
-    // e + w sums stay scalar (their operands straddle the pairs; the DPP
-    // shift still folds into the first).
-    {
+    if constexpr (PK) {
+      // Packed f32 (v_pk_add_f32 / v_pk_fma_f32) on the element pairs 0-1
+      // and 2-3: the same per-element operations in the same order as
+      // stencil() (bitwise equal), ~14.5 VALU per row instead of 24-25; the
+      // horizontal e + w sums stay scalar (their operands straddle the
+      // pairs; the DPP shift still folds into the first).
       typedef float f2 __attribute__((ext_vector_type(2)));
       const f2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
       const f2 ns01 = f2{c[0], c[1]} + f2{a[0], a[1]}, ns23 = f2{c[2], c[3]} + f2{a[2], a[3]};
@@ -123,17 +127,16 @@ struct Upd {
       const f2 r01 = __builtin_elementwise_fma(cy2, ty01, __builtin_elementwise_fma(cx2, tx01, b01));
       const f2 r23 = __builtin_elementwise_fma(cy2, ty23, __builtin_elementwise_fma(cx2, tx23, b23));
       r = vecf{r01[0], r01[1], r23[0], r23[1]};
-    }
-#else
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float w = j == 0 ? wl : b[j - 1];
-      const float e = j == 3 ? er : b[j + 1];
-      // The shifted value as the second operand of e + w (fp add commutes):
-      // the DPP build folds it into v_add_f32_dpp.
-      r[j] = j == 3 ? stencil(b[j], a[j], c[j], e, w, cx, cy) : stencil(b[j], a[j], c[j], w, e, cx, cy);
+      for (int j = 0; j < 4; ++j) {
+        const float w = j == 0 ? wl : b[j - 1];
+        const float e = j == 3 ? er : b[j + 1];
+        // The shifted value as the second operand of e + w (fp add
+        // commutes): the DPP build folds it into v_add_f32_dpp.
+        r[j] = j == 3 ? stencil(b[j], a[j], c[j], e, w, cx, cy) : stencil(b[j], a[j], c[j], w, e, cx, cy);
+      }
     }
-#endif
     if constexpr (MODE == kTileGeneric) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] = (cm[j] && row_ok) ? r[j] : b[j];
@@ -307,7 +310,8 @@ struct Tile {
       const vecf outside = i == 0 ? first_nb : last_nb;
       const vecf n = r == 0 ? outside : (DOWN ? prev : u[r - 1]);
       const vecf so = r == R - 1 ? outside : (DOWN ? u[r + 1] : prev);
-      u[r] = up.apply(n, cur, so, wl[r], er[r], (rowmask >> r) & 1u);
+      u[r] = up.template apply<(R <= kTilePkRows && RES == 0)>(n, cur, so, wl[r], er[r],
+                                                                (rowmask >> r) & 1u);
       if (i == 0) xc.publish(0, u[r]);
       if (i == R - 1) xc.publish(1, u[r]);
       if constexpr (WHAT == 3) sink->row(r, u[r], cur);
