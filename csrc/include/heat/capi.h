@@ -184,13 +184,15 @@ int heat_op_tb_step(const float* src, float* dst, int64_t pitch, int64_t gx0, in
                     int res_level /* residual step 1..depth, 0 = depth */);
 /* TB launch-planner knobs (heat::gpu::TbTuning); weights: up to 4 age-group shares;
    tile_rows / tile_waves: rows per wave / waves per workgroup of tile launches
-   (0 = planner); tile_xl: tile lane shifts 0 DPP, 1 ds_bpermute, 2 mixed (-1 = default). */
+   (0 = planner); tile_xl: tile lane shifts 0 DPP, 1 ds_bpermute, 2 mixed (-1 = default);
+   nt: level-split rows non-temporal 1 / plain 0 (-1 = by the bytes a pass sweeps). */
 typedef struct heat_tb_tuning {
   int32_t variant, rounds, min_len, waves;
   double edge_frac;
   int32_t n_weights, tile_rows;
   double weights[4];
   int32_t tile_waves, tile_xl;
+  int32_t nt, pad_;
 } heat_tb_tuning;
 int heat_tb_get_tuning(heat_tb_tuning* out);
 int heat_tb_set_tuning(const heat_tb_tuning* in);

@@ -198,6 +198,8 @@ struct TbTuning {
                            // 2 mixed (-1: mixed unless the variant has kTileDpp)
   int tile_max_srps = 64;  // HEAT_TB_TILE_MAX: workgroup tiles below this many strip-rows
                            // per SIMD (the automatic variant and Solver::tile_sized)
+  int nt = -1;             // HEAT_TB_NT: level-split rows non-temporal (1) or plain (0);
+                           // -1: non-temporal when a pass sweeps > kTbStreamBytes
   int res_diag = 0;        // HEAT_TB_RES_DIAG: resident-tile timing diagnostics (bits 0-2
                            // give WRONG results): bit 0 no neighbour wait, 1 no ghost reload,
                            // 2 no publish; bit 3 every tile on the masked (edge) path

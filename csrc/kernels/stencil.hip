@@ -301,6 +301,7 @@ TbTuning tuning_from_env() {
   t.tile_waves = std::max(0, geti("HEAT_TB_TILE_WAVES", 0));
   t.tile_xl = geti("HEAT_TB_TILE_XL", -1);
   t.res_diag = geti("HEAT_TB_RES_DIAG", 0) & 15;
+  t.nt = geti("HEAT_TB_NT", -1);
   t.tile_max_srps = std::max(0, geti("HEAT_TB_TILE_MAX", 64));
   if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);
   if (const char* e = std::getenv("HEAT_TB_AGE_WEIGHTS"); e && *e) {
@@ -488,6 +489,11 @@ bool tb_mid_residual(int depth) {
   // take a residual at any inner step; forced variants keep the last step.
   return depth == kTbDeepDepth && tb_tuning().variant < 0;
 }
+
+// Field bytes one pass must sweep before the level-split launches stream
+// their rows (kTbStreamRows): 3/4 of the 256 MB MALL (4096 x 8192 = 134 MB
+// measured faster plain, 8192^2 = 268 MB non-temporal).
+constexpr int64_t kTbStreamBytes = int64_t(192) << 20;
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
@@ -749,16 +755,26 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     }
   }
   const bool split = tb_variant_split(variant);
+  if (split && !(variant & tbv::kShiftMixed)) {
+    // Streaming rows when one pass sweeps more field than the MALL (256 MB)
+    // holds: its rows come back one sweep later, never from L2 or the MALL.
+    int64_t bytes = 0;
+    for (int b = 0; b < nbox; ++b)
+      if (!boxes[b].empty()) bytes += boxes[b].rows() * g.pitch * int64_t(sizeof(float));
+    const bool nt = tune.nt >= 0 ? tune.nt != 0 : bytes > kTbStreamBytes;
+    if (nt) args.flags |= tbdetail::kTbStreamRows;
+  }
   if (tb_trace_enabled()) {
     // HEAT_TB_TRACE=1: each distinct plan once on stderr (planner checks).
     char line[320];
     std::snprintf(line, sizeof line,
                   "[heat tb] depth %d variant %d boxes %d strip_rows %lld waves_target %d bpc %d "
-                  "linear %d units %d age_groups %d cum %d,%d,%d,%d chunk0 %d nchunks0 %d\n",
+                  "linear %d units %d age_groups %d cum %d,%d,%d,%d chunk0 %d nchunks0 %d nt %d\n",
                   depth, variant, n, (long long)total_strip_rows, waves_target, bpc,
                   int((args.flags & tbdetail::kTbLinear) != 0), waves, pairs ? G : 0,
                   args.age_cum[1], args.age_cum[2], args.age_cum[3], args.age_cum[4],
-                  args.box[0].chunk_len, args.box[0].nchunks);
+                  args.box[0].chunk_len, args.box[0].nchunks,
+                  int((args.flags & tbdetail::kTbStreamRows) != 0));
     tb_trace_once(line);
   }
   if (const Stamps sb = stamps_of_current_device(); sb.buf) {
@@ -767,8 +783,9 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
                (long long)sb.waves, (long long)need);
     args.stamps = sb.buf;
   }
-  const bool ok = split ? ((variant & tbv::kShiftMixed) ? tbxm::launch_split(args, depth, st)
-                                                        : tbx::launch_split(args, depth, st))
+  const bool ok = split ? ((variant & tbv::kShiftMixed)                ? tbxm::launch_split(args, depth, st)
+                           : (args.flags & tbdetail::kTbStreamRows) ? tbxn::launch_split(args, depth, st)
+                                                                      : tbx::launch_split(args, depth, st))
                   : (variant & tbv::kFloat2) ? tbn::launch(args, depth, lag, st)
                   : (variant & tbv::kScalar) ? tbs::launch(args, depth, lag, st)
                                              : tbp::launch(args, depth, lag, st);

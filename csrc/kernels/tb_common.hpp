@@ -85,6 +85,11 @@ constexpr int kTbDiagCachedRows = 16;
 //                    SIMD gets the same work whatever the shape; a unit may
 //                    run several segments (strip / box / Dirichlet-mode ends).
 constexpr int kTbLinear = 32;
+//   kTbStreamRows    level-split launches take the streaming build
+//                    (tb_split_nt.hip: non-temporal row loads and stores)
+//                    when one pass sweeps more than the MALL holds
+//                    (kTbStreamBytes, HEAT_TB_NT overrides).
+constexpr int kTbStreamRows = 64;
 
 __device__ __forceinline__ bool in_interior(int64_t g, int64_t n) { return g >= 1 && g <= n - 2; }
 
@@ -133,6 +138,9 @@ int occupancy_split(int depth);
 bool launch_split_rl_a(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 bool launch_split_rl_b(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 bool launch_split_rl_c(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
+}
+namespace heat::gpu::tbxn {  // level-split pipelines, non-temporal rows (tb_split_nt.hip)
+bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);
 }
 namespace heat::gpu::tbxm {  // level-split pipelines, mixed DPP / ds_bpermute shifts (tb_split_mixed.hip)
 bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);

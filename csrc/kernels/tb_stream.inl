@@ -38,6 +38,29 @@
 #ifndef HEAT_TB_BUFSTORE
 #define HEAT_TB_BUFSTORE 0
 #endif
+// Row cache policy.  HEAT_TB_NTSTORE / HEAT_TB_NTLOAD 1: non-temporal output
+// stores / input-row loads (the streaming build tb_split_nt.hip, taken when
+// one pass sweeps more than the MALL holds: the rows a pass writes are read
+// back one whole-field sweep later, past L2 and the MALL).  8192^2 bench
+// 5.03-5.09 -> 5.24-5.25 Tcells/s, 131072^2 5.53 -> 5.63; but the 4096 x
+// 8192 plate (134 MB, inside the MALL) 4.76-4.83 -> 4.66-4.70, so the
+// smaller fields keep the plain build (profiles/r5_stores.md).
+// Experiment builds (HEAT_LIB A/B): HEAT_TB_STORE_AUX = the cache-policy
+// bits of the buffer-store build (HEAT_TB_BUFSTORE); HEAT_TB_DIAG_FIXEDSTORE
+// 1 = every store of a unit to one row (the store instructions without the
+// HBM write stream; timing only, wrong results).
+#ifndef HEAT_TB_NTSTORE
+#define HEAT_TB_NTSTORE 0
+#endif
+#ifndef HEAT_TB_NTLOAD
+#define HEAT_TB_NTLOAD 0
+#endif
+#ifndef HEAT_TB_STORE_AUX
+#define HEAT_TB_STORE_AUX 0
+#endif
+#ifndef HEAT_TB_DIAG_FIXEDSTORE
+#define HEAT_TB_DIAG_FIXEDSTORE 0
+#endif
 
 namespace heat::gpu::HEAT_TB_NS {
 
@@ -95,6 +118,15 @@ __device__ __forceinline__ float to_vgpr(float x) {
   float r;
   asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
   return r;
+}
+
+// One input row element of this lane.
+__device__ __forceinline__ vecf ld_in(const float* p) {
+#if HEAT_TB_NTLOAD
+  return __builtin_nontemporal_load(reinterpret_cast<const vecf*>(p));
+#else
+  return *reinterpret_cast<const vecf*>(p);
+#endif
 }
 
 // Dirichlet handling modes (wave-uniform, chosen per wave in tb_kernel).
@@ -250,7 +282,7 @@ struct TbStream {
       return x;
     } else {
       if (cached_rows) row = seq0 + (row & 3);  // diagnostics: cache-resident input
-      return *reinterpret_cast<const vecf*>(src + row * pitch + lo);
+      return ld_in(src + row * pitch + lo);
     }
   }
 
@@ -287,9 +319,9 @@ struct TbStream {
       typedef unsigned uvec __attribute__((ext_vector_type(V)));
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + off, 0, 4 * V * 64, 0x00020000);
 #if HEAT_TB_V == 4
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec, out), rs, vso, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec, out), rs, vso, 0, HEAT_TB_STORE_AUX);
 #else
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec, out), rs, vso, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec, out), rs, vso, 0, HEAT_TB_STORE_AUX);
 #endif
       if constexpr (LASTRES) {
         float d[V];
@@ -303,7 +335,17 @@ struct TbStream {
     }
 #endif
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
+#if HEAT_TB_DIAG_FIXEDSTORE
+      // Diagnostics build: every store of the unit goes to its first output
+      // row (same instructions, L2-resident target: the store issue cost
+      // without the HBM write traffic; wrong results).
+      off = rb * pitch;
+#endif
+#if HEAT_TB_NTSTORE
+      if (!nostore) __builtin_nontemporal_store(out, reinterpret_cast<vecf*>(dst + off + lo));
+#else
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
+#endif
       if constexpr (LASTRES) {
         // max |delta| with the NaN-propagating IEEE-2019 maximum
         // (v_maximum3_f32, abs folded into its inputs): a NaN or inf
@@ -346,7 +388,7 @@ struct TbStream {
       vecf c = P[U];
       {
         const int64_t nxt = min(i + RING, last_in);
-        P[U] = *reinterpret_cast<const vecf*>(src + nxt * pitch + lo);
+        P[U] = ld_in(src + nxt * pitch + lo);
       }
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -405,7 +447,7 @@ struct TbStream {
                                         int64_t* roff, int64_t* woff) {
     // Row t + 3 into the slot of row t - 3 (level 1 now reads t-2 .. t).
     if constexpr (FAST && ROLE != 2) {
-      L0[modn<6>(T6 + 3)] = *reinterpret_cast<const vecf*>(src + *roff + lo);
+      L0[modn<6>(T6 + 3)] = ld_in(src + *roff + lo);
       *roff += pitch;
     } else {
       L0[modn<6>(T6 + 3)] = load_row(src, FAST ? i + 3 : min(i + 3, last_in), pitch);

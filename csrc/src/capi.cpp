@@ -491,6 +491,7 @@ int heat_tb_get_tuning(heat_tb_tuning* out) {
     out->tile_rows = t.tile_rows;
     out->tile_waves = t.tile_waves;
     out->tile_xl = t.tile_xl;
+    out->nt = t.nt;
     out->n_weights = int32_t(std::min<size_t>(t.age_weights.size(), 4));
     for (int i = 0; i < out->n_weights; ++i) out->weights[i] = t.age_weights[size_t(i)];
   });
@@ -509,6 +510,7 @@ int heat_tb_set_tuning(const heat_tb_tuning* in) {
     t.tile_rows = std::max(0, in->tile_rows);
     t.tile_waves = std::max(0, in->tile_waves);
     t.tile_xl = in->tile_xl;
+    t.nt = in->nt;
     t.age_weights.assign(in->weights, in->weights + in->n_weights);
     heat::gpu::tb_set_tuning(t);
   });

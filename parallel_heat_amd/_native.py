@@ -108,7 +108,7 @@ class HeatTbTuning(Structure):
     _fields_ = [("variant", c_int32), ("rounds", c_int32), ("min_len", c_int32),
                 ("waves", c_int32), ("edge_frac", c_double), ("n_weights", c_int32),
                 ("tile_rows", c_int32), ("weights", c_double * 4), ("tile_waves", c_int32),
-                ("tile_xl", c_int32)]
+                ("tile_xl", c_int32), ("nt", c_int32), ("pad_", c_int32)]
 
 
 class HeatChecksum(Structure):

@@ -64,6 +64,7 @@ class TbTuning:
     tile_rows: int = 0  # rows per wave of TILE launches (0: planner)
     tile_waves: int = 0  # waves per TILE workgroup, 8 or 16 (0: planner)
     tile_xl: int = -1  # TILE lane shifts: 0 DPP, 1 ds_bpermute, 2 mixed (-1: default)
+    nt: int = -1  # level-split rows non-temporal 1 / plain 0 (-1: by the bytes a pass sweeps)
 
 
 def tb_tuning() -> TbTuning:
@@ -71,7 +72,7 @@ def tb_tuning() -> TbTuning:
     _native.call("heat_tb_get_tuning", ctypes.byref(t))
     return TbTuning(t.variant, t.rounds, t.min_len, t.waves, t.edge_frac,
                     [t.weights[i] for i in range(t.n_weights)], t.tile_rows, t.tile_waves,
-                    t.tile_xl)
+                    t.tile_xl, t.nt)
 
 
 def set_tb_tuning(t: TbTuning) -> None:
@@ -81,7 +82,7 @@ def set_tb_tuning(t: TbTuning) -> None:
     c = _native.HeatTbTuning(int(t.variant), int(t.rounds), int(t.min_len), int(t.waves),
                              float(t.edge_frac), n, int(t.tile_rows),
                              (ctypes.c_double * 4)(*t.age_weights), int(t.tile_waves),
-                             int(t.tile_xl))
+                             int(t.tile_xl), int(t.nt), 0)
     _native.call("heat_tb_set_tuning", ctypes.byref(c))
 
 

@@ -384,3 +384,37 @@ def test_tb_split_mixed_shifts_bitwise(gpu, depth, variant):
         ref = _cpu_steps(g, lx, ly, depth, depth)
         assert torch.equal(b.owned().cpu(), ref), (lx, ly)
         assert ops.resid_value(resid) == float((ref - prev).abs().max())
+
+
+@pytest.mark.parametrize("variant,depth", [(DEEP, 12), (DEEP, 8), (DEEP | V.ALT_DIRECTION, 12),
+                                           (DEEP | V.FORCE_AGE_PAIRS, 12), (DEEP | V.LINEAR, 12)])
+def test_tb_split_streaming_rows_bitwise(gpu, depth, variant):
+    # tb_split_nt.hip (non-temporal row loads / stores, taken above
+    # kTbStreamBytes per pass): forced on small plates through the tuning
+    # knob, bitwise vs the CPU oracle with the residual; an inner-level check
+    # (the plain rl units) under the same knob.
+    saved = ops.tb_tuning()
+    try:
+        t = ops.tb_tuning()
+        t.nt = 1
+        ops.set_tb_tuning(t)
+        for lx, ly in ((203, 517), (1000, 2000)):
+            g, a, b = _fields(lx, ly, depth, gpu)
+            resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+            ops.tb_step(a, b, g, depth, resid=resid, variant=variant)
+            torch.cuda.synchronize()
+            prev = _cpu_steps(g, lx, ly, depth, depth - 1)
+            ref = _cpu_steps(g, lx, ly, depth, depth)
+            assert torch.equal(b.owned().cpu(), ref), (lx, ly)
+            assert ops.resid_value(resid) == float((ref - prev).abs().max())
+        if depth == 12 and variant == DEEP:
+            g, a, b = _fields(1000, 2000, 12, gpu)
+            resid = torch.zeros(1, dtype=torch.int32, device=gpu)
+            ops.tb_step(a, b, g, 12, resid=resid, variant=variant, res_level=10)
+            torch.cuda.synchronize()
+            l9 = _cpu_steps(g, 1000, 2000, 12, 9)
+            l10 = _cpu_steps(g, 1000, 2000, 12, 10)
+            assert torch.equal(b.owned().cpu(), _cpu_steps(g, 1000, 2000, 12, 12))
+            assert ops.resid_value(resid) == float((l10 - l9).abs().max())
+    finally:
+        ops.set_tb_tuning(saved)

@@ -9,7 +9,7 @@ def test_tuning_roundtrip():
     saved = ops.tb_tuning()
     try:
         t = ops.TbTuning(variant=int(ops.TbVariant.DEFAULT), rounds=2, min_len=24, waves=512,
-                         edge_frac=0.75, age_weights=[1.5, 1.0], tile_rows=16, tile_waves=8)
+                         edge_frac=0.75, age_weights=[1.5, 1.0], tile_rows=16, tile_waves=8, nt=1)
         ops.set_tb_tuning(t)
         assert ops.tb_tuning() == t
         with pytest.raises(ValueError):
