@@ -63,8 +63,8 @@ STREAM_POINTS: List[tuple] = [
     (18.0, 3.0),    # extrapolated, unmeasured
     (36.0, 3.3),    # 1024 x 8192 per-pass tiles (round 3/4: 3.23)
     (72.0, 3.90),   # 2048 x 8192 3.90 / 4096 x 4096 3.90, split pipelines
-    (144.0, 4.9),   # 4096 x 8192 4.91 (2 GPUs)
-    (288.0, 5.05),  # 8192 x 8192 5.03-5.21 (1 GPU)
+    (144.0, 4.85),  # 4096 x 8192 4.76-4.91 (2 GPUs, plain rows)
+    (288.0, 5.15),  # 8192 x 8192 5.13-5.25 (1 GPU, streaming rows, profiles/r5_stores.md)
 ]
 RATE_POINTS = STREAM_POINTS  # the large-block end (1 GPU) is a stream plate
 
