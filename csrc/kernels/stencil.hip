@@ -300,7 +300,7 @@ TbTuning tuning_from_env() {
   t.tile_rows = std::max(0, geti("HEAT_TB_TILE_ROWS", 0));
   t.tile_waves = std::max(0, geti("HEAT_TB_TILE_WAVES", 0));
   t.tile_xl = geti("HEAT_TB_TILE_XL", -1);
-  t.res_diag = geti("HEAT_TB_RES_DIAG", 0) & 15;
+  t.res_diag = geti("HEAT_TB_RES_DIAG", 0) & 31;
   t.nt = geti("HEAT_TB_NT", -1);
   t.tile_max_srps = std::max(0, geti("HEAT_TB_TILE_MAX", 64));
   if (const char* e = std::getenv("HEAT_TB_EDGE_FRAC"); e && *e) t.edge_frac = std::atof(e);

@@ -34,7 +34,8 @@ struct ResArgs {
   int chk_pass[kResMaxChecks], chk_step[kResMaxChecks];
   int diag;             // timing diagnostics (HEAT_TB_RES_DIAG; bits 0-2 give wrong
                         // results): bit 0 no neighbour wait, 1 no ghost reload, 2 no
-                        // publish, 3 every tile on the masked path
+                        // publish, 3 every tile on the masked path, 4 plate edge rows
+                        // computed as interior rows (what the masked edge waves cost)
 };
 
 // Neighbour waits give up after this many polls (~0.3 s with s_sleep 2).
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   // This wave's global rows (the mode is per wave, see tile_mode).
   const int64_t wx_lo = g.gx0 + ub - K + int64_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * R;
   const int64_t wx_hi = wx_lo + R - 1;
-  const int mode = (ra.diag & 8) ? kTileGeneric : tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi);
+  const int mode = (ra.diag & 8) ? kTileGeneric : tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi, ra.diag & 16);
   tile_dispatch<XL>(mode, [&](auto mode_c) {
     resident_run<R, NW, decltype(mode_c)::value, XL, RES>(ra, bx, strip, t, blk, xch);
     return 0.f;

@@ -155,8 +155,9 @@ struct TileNoSink;
 // columns [gy_lo, gy_hi].  Lanes hold 4 columns starting at a global column
 // = gy0 (mod 4).
 __device__ __forceinline__ int tile_mode(const StencilGeom& g, int64_t wx_lo, int64_t wx_hi,
-                                         int64_t gy_lo, int64_t gy_hi) {
-  const bool edge_row = (wx_lo <= 0 && 0 <= wx_hi) || (wx_lo <= g.nx - 1 && g.nx - 1 <= wx_hi);
+                                         int64_t gy_lo, int64_t gy_hi, bool no_edge_rows = false) {
+  const bool edge_row = !no_edge_rows &&
+                        ((wx_lo <= 0 && 0 <= wx_hi) || (wx_lo <= g.nx - 1 && g.nx - 1 <= wx_hi));
   const bool left = gy_lo < 1, right = gy_hi > g.ny - 2;
   if (edge_row || (left && right)) return kTileGeneric;
   if (!left && !right) return kTileInterior;
