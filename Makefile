@@ -36,7 +36,7 @@ $(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o $(BUILD)
   $(BUILD)/obj/tb_tile_xl0.o $(BUILD)/obj/tb_tile_xl1.o $(BUILD)/obj/tb_tile_xl2.o \
   $(BUILD)/obj/tb_resident_xl0.o $(BUILD)/obj/tb_resident_xl1.o $(BUILD)/obj/tb_resident_xl2.o \
   $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o \
-  $(BUILD)/obj/tb_split_mixed.o $(BUILD)/obj/tb_split_nt.o: HIPFLAGS += -fno-slp-vectorize
+  $(BUILD)/obj/tb_split_mixed.o $(BUILD)/obj/tb_split_nt.o $(BUILD)/obj/tb_chain.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)

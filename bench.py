@@ -469,7 +469,8 @@ def explain_run(cfg, info, shared, world, iters, HeatSolver, xgmi=None):
                       "compute": round(r.t_compute * scale, 6),
                       "reduce": round(r.t_reduce * scale, 6),
                       "wall": round(r.seconds * scale, 6),
-                      "resident_passes": r.resident_passes}
+                      "resident_passes": r.resident_passes,
+                      "chained_passes": r.chained_passes}
     except Exception as e:  # noqa: BLE001 - diagnostics only; every rank still gathers
         phases["error"] = str(e)[:200]
     every = [None] * world

@@ -66,6 +66,7 @@ typedef struct heat_run_stats {
   double t_exchange, t_compute, t_reduce; /* seconds per phase (phase_timing) */
   int64_t resident_passes;                /* passes run inside resident-tile launches */
   int64_t resident_giveups;               /* 1: a resident launch gave up (HEAT_TB_RES_GIVEUP=defer) */
+  int64_t chained_passes;                 /* passes run inside chained level-split launches */
 } heat_run_stats;
 
 typedef struct heat_block_info {

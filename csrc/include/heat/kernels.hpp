@@ -125,9 +125,23 @@ void mfma_step(const float* src, float* dst, const StencilGeom& g, const Box& bo
 
 // res_level (with resid): the step 1..depth whose max |new - old| is taken;
 // 0 = depth (the pass's last step).  Inner levels need tb_mid_residual(depth).
+// chain (optional): run chain->passes passes of `depth` steps in ONE launch
+// of the chained level-split kernel (tb_chain.hip) when this launch's plan
+// qualifies (the streaming split build, one box, no residual, a classic
+// plan of one dispatch round, at most chain->max_units units); the passes
+// ping-pong between src and dst (an odd count ends in dst).  chain->chained
+// reports whether it ran; if not, nothing was launched.
+struct TbChain {
+  int passes = 1;
+  unsigned* flags = nullptr;  // >= max_units words, zero (the launch re-zeroes them)
+  unsigned* done = nullptr;   // zero (re-zeroed by the launch)
+  unsigned* err = nullptr;    // set non-zero if a unit's poll gave up
+  int max_units = 0;
+  bool chained = false;
+};
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target = 0, int variant = -1,
-             int res_level = 0);
+             int res_level = 0, TbChain* chain = nullptr);
 // Resident workgroup tiles (tb_resident.hip): `passes` passes of `depth`
 // steps over ONE box in a single launch whose tiles stay in VGPRs, trading
 // only their K-deep ghost rings between passes through two exchange fields

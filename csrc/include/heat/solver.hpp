@@ -57,6 +57,7 @@ struct RunStats {
   // summed over launches, so concurrent phases may add up to > seconds).
   double t_exchange = 0.0, t_compute = 0.0, t_reduce = 0.0;
   int64_t resident_passes = 0;  // passes run inside resident-tile launches
+  int64_t chained_passes = 0;   // passes run inside chained level-split launches
   // 1: a resident launch of this call gave up a neighbour wait (results
   // invalid; only returned with HEAT_TB_RES_GIVEUP=defer, else run throws).
   int64_t resident_giveups = 0;
@@ -183,6 +184,11 @@ class Solver {
   int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
   static int device_users(int dev);  // live GPU solvers of this process on dev
   void enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int n);
+  // Chained passes (one-rank runs of the streaming level-split build): the
+  // unchecked depth-T_ passes from plan[i] on, run as one launch; false if
+  // tb_step's plan did not qualify (chained passes then stay off).
+  int chain_span(const std::vector<PassPlan>& plan, size_t i) const;
+  bool enqueue_chain(const std::vector<PassPlan>& plan, size_t i0, int n);
   RunStats run_impl(int64_t steps, bool wait);
   RunStats run_guarded(int64_t steps, bool wait);
   void complete_pending();  // run(0) if an enqueue()d run is in flight
@@ -230,6 +236,7 @@ class Solver {
   bool host_checks_ = false;
   bool warmed_ = false;    // RCCL connections established outside capture
   bool resident_ = false;  // resident-tile launches enabled for this solver
+  bool chain_ = false;     // chained level-split passes (HEAT_TB_CHAIN=1; off by default)
   bool resident_force_ = false;  // HEAT_TB_RESIDENT=2: also with ranks sharing the device
   bool resident_used_ = false;  // one was enqueued in this run (check its error word)
   bool pending_ = false;         // an enqueue()d run not yet completed by run()
@@ -246,7 +253,7 @@ class Solver {
   int cur_ = 0;
   int64_t step_ = 0;
   float cpu_resid_ = 0.f;
-  int64_t stat_passes_ = 0, stat_exchanges_ = 0, stat_resident_ = 0;
+  int64_t stat_passes_ = 0, stat_exchanges_ = 0, stat_resident_ = 0, stat_chained_ = 0;
 
   float* base_[2] = {nullptr, nullptr};
   float* field_[2] = {nullptr, nullptr};
@@ -278,6 +285,7 @@ class Solver {
     int64_t passes = 0, exchanges = 0;
     bool resident = false;         // holds a resident-tile launch (check its error word)
     int64_t resident_passes = 0;
+    int64_t chained_passes = 0;
     std::vector<PassRec> recs;     // relative to the segment's first step
     std::vector<int64_t> checks;   // check steps (relative), in judge order
   };

@@ -436,6 +436,10 @@ int tb_auto_variant(int depth, int64_t strip_rows_per_simd) {
   if (depth >= 4 && depth % 2 == 0 && strip_rows_per_simd < tb_tuning().tile_max_srps)
     return tbv::kTile | tbv::kXcdGroups;
   if (depth == kTbDeepDepth && strip_rows_per_simd < 64) return tbv::kDefault;
+  // Depth 8 on whole-GPU plates (the remainder passes of 1000 = 82 x 12 +
+  // 8 + 8 at 8192^2: 288 strip-rows per SIMD) as split pipelines too:
+  // bench 5.21-5.22 vs 5.19-5.21 interleaved (profiles/r5_stores.md).
+  if (depth == 8 && strip_rows_per_simd >= 256) return tbv::kDefaultDeep;
   return tb_default_variant(depth);
 }
 
@@ -497,7 +501,8 @@ constexpr int64_t kTbStreamBytes = int64_t(192) << 20;
 
 void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxes, int nbox,
              int depth, unsigned* resid, hipStream_t st, int waves_target, int variant,
-             int res_level) {
+             int res_level, TbChain* chain) {
+  if (chain) chain->chained = false;
   HEAT_CHECK(nbox >= 0 && nbox <= 5, "nbox=%d", nbox);  // API limit (5 boxes)
   HEAT_CHECK(res_level >= 0 && res_level <= depth, "residual level %d of a depth-%d pass",
              res_level, depth);
@@ -782,6 +787,41 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     HEAT_CHECK(need <= sb.waves, "stamp buffer holds %lld waves, launch has %lld",
                (long long)sb.waves, (long long)need);
     args.stamps = sb.buf;
+  }
+  if (chain && chain->passes > 1) {
+    // Chained passes: the streaming build's classic one-box plan of one
+    // dispatch round (every unit resident: the units poll each other).
+    // args.total_waves counts the units of one age group (launch_chain).
+    const int G = (args.flags & tbdetail::kTbAgePairs) ? args.age_groups : 1;
+    int blocks = (args.total_waves + 1) / 2;
+    if (G > 1) blocks = (blocks + 7) / 8 * 8 * G;
+    static int occ = -1;  // one device model per process (gfx950)
+    if (occ < 0) occ = tbc::occupancy_chain(kTbDeepDepth);
+    int dev = 0, cus = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const bool fits = split && !(variant & tbv::kShiftMixed) && (args.flags & tbdetail::kTbStreamRows) &&
+                      !(args.flags & tbdetail::kTbLinear) && !(args.flags & tbdetail::kTbAltDirection) &&
+                      n == 1 && resid == nullptr && depth == kTbDeepDepth && args.stamps == nullptr &&
+                      int64_t(args.total_waves) * G <= chain->max_units && blocks <= cus * occ;
+    if (tb_trace_enabled()) {
+      char line[320];
+      std::snprintf(line, sizeof line,
+                    "[heat chain] passes %d split %d mixed %d stream %d linear %d alt %d boxes %d resid %d "
+                    "depth %d units %d x %d max %d blocks %d cus %d occ %d -> %d\n",
+                    chain->passes, int(split), int((variant & tbv::kShiftMixed) != 0),
+                    int((args.flags & tbdetail::kTbStreamRows) != 0),
+                    int((args.flags & tbdetail::kTbLinear) != 0),
+                    int((args.flags & tbdetail::kTbAltDirection) != 0), n, int(resid != nullptr), depth,
+                    args.total_waves, G, chain->max_units, blocks, cus, occ, int(fits));
+      tb_trace_once(line);
+    }
+    if (fits) {
+      chain->chained = tbc::launch_chain(args, depth, chain->passes, chain->flags, chain->done,
+                                         chain->err, st);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
   }
   const bool ok = split ? ((variant & tbv::kShiftMixed)                ? tbxm::launch_split(args, depth, st)
                            : (args.flags & tbdetail::kTbStreamRows) ? tbxn::launch_split(args, depth, st)

@@ -139,6 +139,11 @@ bool launch_split_rl_a(const tbdetail::TbArgs& args, int depth, int rl, hipStrea
 bool launch_split_rl_b(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 bool launch_split_rl_c(const tbdetail::TbArgs& args, int depth, int rl, hipStream_t st);
 }
+namespace heat::gpu::tbc {  // chained level-split passes (tb_chain.hip)
+int occupancy_chain(int depth);
+bool launch_chain(const tbdetail::TbArgs& args, int depth, int passes, unsigned* flags, unsigned* done,
+                  unsigned* err, hipStream_t st);
+}
 namespace heat::gpu::tbxn {  // level-split pipelines, non-temporal rows (tb_split_nt.hip)
 bool launch_split(const tbdetail::TbArgs& args, int depth, hipStream_t st);
 }

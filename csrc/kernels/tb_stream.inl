@@ -55,6 +55,30 @@
 #ifndef HEAT_TB_NTLOAD
 #define HEAT_TB_NTLOAD 0
 #endif
+// Chained level-split passes (tb_chain.hip, tb_chain_kernel): the cache
+// policy of their write-through stores (16 = sc1).
+#ifndef HEAT_TB_CHAIN
+#define HEAT_TB_CHAIN 0
+#endif
+#ifndef HEAT_TB_CHAIN_AUX
+#define HEAT_TB_CHAIN_AUX 16
+#endif
+// s_sleep argument between a chained unit's flag polls; HEAT_TB_CHAIN_NOWAIT
+// 1 (diagnostics, wrong results) skips the waits.
+#ifndef HEAT_TB_CHAIN_SLEEP
+#define HEAT_TB_CHAIN_SLEEP 1
+#endif
+#ifndef HEAT_TB_CHAIN_NOWAIT
+#define HEAT_TB_CHAIN_NOWAIT 0
+#endif
+// Diagnostics: the chained build with the streaming build's non-temporal
+// stores (not write-through: valid only with HEAT_TB_CHAIN_NOWAIT timing).
+#ifndef HEAT_TB_CHAIN_NTSTORE
+#define HEAT_TB_CHAIN_NTSTORE 0
+#endif
+#if HEAT_TB_CHAIN && (HEAT_TB_V != 4 || HEAT_TB_BUFSTORE)
+#error "the chained build stores float4 rows through buffer stores of its own"
+#endif
 #ifndef HEAT_TB_STORE_AUX
 #define HEAT_TB_STORE_AUX 0
 #endif
@@ -341,7 +365,16 @@ struct TbStream {
       // without the HBM write traffic; wrong results).
       off = rb * pitch;
 #endif
-#if HEAT_TB_NTSTORE
+#if HEAT_TB_CHAIN && !HEAT_TB_CHAIN_NTSTORE
+      // Chained passes: write-through (sc1) 16-B stores, so a neighbour
+      // unit on another XCD reads them after this unit's flag (drained
+      // stores, then an sc1 flag store; tb_chain_kernel).
+      if (!nostore) {
+        typedef unsigned uvec __attribute__((ext_vector_type(V)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + off, 0, 4 * V * 64, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec, out), rs, 4 * lo, 0, HEAT_TB_CHAIN_AUX);
+      }
+#elif HEAT_TB_NTSTORE
       if (!nostore) __builtin_nontemporal_store(out, reinterpret_cast<vecf*>(dst + off + lo));
 #else
       if (!nostore) *reinterpret_cast<vecf*>(dst + off + lo) = out;
@@ -651,7 +684,9 @@ __device__ __forceinline__ int tb_unit(const TbArgs& a, int per_block, int sub, 
 template <int K, int LAG, int K1, int RLM = 0>
 __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, int strip,
                                                int chunk, int64_t rb, int64_t re, int stage,
-                                               vecf* ring, unsigned* cnt, int64_t qoff) {
+                                               vecf* ring, unsigned* cnt, int64_t qoff,
+                                               const float* sbase = nullptr,
+                                               float* dbase = nullptr) {
   constexpr int KK = (K + V - 1) / V * V;  // strip overlap per side, whole lanes
   constexpr int W = 64 * V - 2 * KK;
   constexpr int K2 = K - K1;               // levels of stage 1
@@ -662,8 +697,10 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
   const bool store_lane = col >= cbase && col < cend;
 
   const StencilGeom& g = a.g;
-  const float* src = a.src + (cbase - KK);  // wave-uniform; + lo per lane
-  float* dst = a.dst + (cbase - KK);
+  // wave-uniform; + lo per lane.  sbase / dbase: the chained launch's
+  // ping-pong fields of the current pass (tb_chain_kernel).
+  const float* src = (sbase ? sbase : a.src) + (cbase - KK);
+  float* dst = (dbase ? dbase : a.dst) + (cbase - KK);
   int64_t pitch = g.pitch;
   const bool want_resid = a.resid != nullptr;
 
@@ -945,6 +982,144 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_sp
 }
 #endif
 
+#if HEAT_TB_SPLIT && HEAT_TB_CHAIN
+// Chained level-split passes (tb_chain.hip): ONE launch runs `passes`
+// depth-K passes of a one-box classic plan, ping-ponging between a.src and
+// a.dst, with no grid-wide boundary between passes.  A per-pass launch ends
+// when its slowest pipeline does (busy fraction 0.81 at 8192^2: the waves of
+// a pass end between 135 and 184 us, tools/wave_timeline.py); here a unit
+// starts pass p as soon as the units whose rows it reads (and will
+// overwrite) finished pass p - 1, and a waiting wave leaves its SIMD's issue
+// slots to the waves beside it.
+//   unit u = (strip s, chunk group c, age a); flags[u] = passes it finished.
+//   Stage 1 (the only wave that stores the unit's rows) drains its sc1
+//   stores (s_waitcnt vmcnt(0)), then one lane stores flags[u] = p + 1
+//   (sc1, relaxed, agent scope).
+//   Stage 0, before pass p >= 1, polls (sc1 loads) the flags of every unit
+//   of strips s-1..s+1, groups c-1..c+1, all ages (itself included) until
+//   they reach p: their pass p - 1 rows are stored (RAW) and their pass p - 1
+//   reads of the field this pass overwrites are done (WAR: a unit's stage 0
+//   finishes reading before its stage 1 finishes).  Row loads are
+//   non-temporal (they bypass the CU's L1, the only cache that could hold a
+//   stale copy; MI355X_MICROARCH inter-workgroup visibility).
+//   Bounded polls: a give-up sets *err (grid not co-resident) and the run is
+//   reported invalid by the solver, as for resident tiles.
+//   The last unit to finish re-zeroes the flags and the counter.
+struct ChainArgs {
+  int passes;
+  unsigned* flags;  // one word per unit (total_waves x age groups), zero at launch
+  unsigned* done;   // units finished (zero at launch)
+  unsigned* err;    // non-zero: a poll gave up
+};
+constexpr unsigned kChainSpinLimit = 1u << 22;
+
+template <int K, int K1>
+__global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_chain_kernel(TbArgs a,
+                                                                                        ChainArgs c) {
+  constexpr int K2 = K - K1;
+  __shared__ vecf ring[2][kSplitRing * 64];
+  __shared__ unsigned cnt[2][2];
+  if (tbdetail::gated(a.g.gate)) return;  // uniform over the launch: nobody waits
+  if (threadIdx.x < 4) cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __syncthreads();
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pp = wid >> 1, stage = wid & 1;
+  const int lane = threadIdx.x & 63;
+  int age = 0;
+  const int unit = tb_unit(a, 2, pp, age);
+  const bool pairs = a.flags & tbdetail::kTbAgePairs;
+  const int G = pairs ? a.age_groups : 1;
+  const unsigned nunits = unsigned(a.total_waves) * unsigned(G);
+  if (unit < a.total_waves) {
+    const TbBox& bx = a.box[0];
+    const int strip = unit % bx.nstrips, chunk = unit / bx.nstrips;
+    const int ngroups = a.total_waves / bx.nstrips;
+    int64_t rb = bx.r0 + int64_t(chunk) * bx.chunk_len;
+    int64_t re = min(rb + bx.chunk_len, bx.r1);
+    if (pairs) {
+      const int64_t p0 = bx.r0 + int64_t(chunk) * G * bx.chunk_len;
+      const int64_t p1 = min(p0 + G * int64_t(bx.chunk_len), bx.r1);
+      rb = p0 + ((p1 - p0) * a.age_cum[age]) / 1024;
+      re = p0 + ((p1 - p0) * a.age_cum[age + 1]) / 1024;
+    }
+    const int fid = unit + age * a.total_waves;
+    // Stage 0: lane l < 9 G watches unit (s + l%3 - 1, c + (l/3)%3 - 1, age l/9).
+    int nf = -1;
+    if (stage == 0 && lane < 9 * G) {
+      const int q = lane % 9, ag = lane / 9;
+      const int s2 = strip + q % 3 - 1, c2 = chunk + q / 3 - 1;
+      if (s2 >= 0 && s2 < bx.nstrips && c2 >= 0 && c2 < ngroups)
+        nf = c2 * bx.nstrips + s2 + ag * a.total_waves;
+    }
+    const float* src = a.src;
+    float* dst = a.dst;
+    int64_t qoff = 0;
+    for (int p = 0; p < c.passes; ++p) {
+      if (stage == 0 && p > 0 && !HEAT_TB_CHAIN_NOWAIT) {
+        for (unsigned spins = 0;; ++spins) {
+          const unsigned v =
+              nf >= 0 ? __hip_atomic_load(c.flags + nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : unsigned(p);
+          if (__all(v >= unsigned(p))) break;
+          if (spins >= kChainSpinLimit) {
+            if (lane == 0) __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(HEAT_TB_CHAIN_SLEEP);
+        }
+      }
+      if (rb < re)
+        (void)tb_segment<K, 3, K1>(a, bx, strip, chunk, rb, re, stage, ring[pp], cnt[pp], qoff, src,
+                                   dst);
+      qoff += (re - rb) + 2 * K2;
+      if (stage == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(c.flags + fid, unsigned(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const float* t = src;
+      src = dst;
+      dst = const_cast<float*>(t);
+    }
+    if (stage == 1 && lane == 0) {
+      // Every other unit is past its last poll once the counter reaches
+      // nunits: the last one re-zeroes the flags for the next launch.
+      const unsigned n = __hip_atomic_fetch_add(c.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (n + 1 == nunits) {
+        for (unsigned i = 0; i < nunits; ++i)
+          __hip_atomic_store(c.flags + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(c.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+template <int K, int K1>
+int occ_chain_k() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, tb_chain_kernel<K, K1>, 256, 0) != hipSuccess) n = 0;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tb_chain_kernel<K, K1>)) == hipSuccess &&
+      fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    n = std::min(n, std::min(8, 512 / alloc));
+  }
+  return std::max(0, n);
+}
+// Blocks per CU the chained kernel keeps resident (0: not built for depth).
+int occupancy_chain(int depth) { return depth == 12 ? occ_chain_k<12, 6>() : 0; }
+// One launch of `passes` chained depth-12 passes (classic plan, one box).
+bool launch_chain(const TbArgs& args, int depth, int passes, unsigned* flags, unsigned* done,
+                  unsigned* err, hipStream_t st) {
+  if (depth != 12) return false;
+  int blocks = int((args.total_waves + 1) / 2);
+  if (args.flags & tbdetail::kTbAgePairs) blocks = (blocks + 7) / 8 * 8 * args.age_groups;
+  ChainArgs c{passes, flags, done, err};
+  hipLaunchKernelGGL((tb_chain_kernel<12, 6>), dim3(blocks), dim3(256), 0, st, args, c);
+  return true;
+}
+#endif
+
 #ifndef HEAT_TB_EXPERIMENT  // experiments instantiate tb_kernel<K, LAG> themselves
 template <int K, int LAG>
 void launch_k(const TbArgs& args, hipStream_t st) {
@@ -1050,7 +1225,7 @@ bool launch(const TbArgs& args, int depth, int lag, hipStream_t st) {
 
 #endif  // !HEAT_TB_SPLIT_RL_LO
 
-#if HEAT_TB_SPLIT
+#if HEAT_TB_SPLIT && !HEAT_TB_CHAIN
 template <int K, int K1, int RLM = 0, int LIN = 2>
 void launch_split_k(const TbArgs& args, hipStream_t st) {
   int blocks = int((args.total_waves + 1) / 2);  // two pipelines per block
@@ -1078,7 +1253,7 @@ bool HEAT_TB_SPLIT_RL_FN(const TbArgs& args, int depth, int rl, hipStream_t st) 
   return depth == 12 && launch_split_rl_range<HEAT_TB_SPLIT_RL_LO>(args, rl, st);
 }
 #endif
-#if HEAT_TB_SPLIT && !HEAT_TB_SPLIT_RL_LO
+#if HEAT_TB_SPLIT && !HEAT_TB_SPLIT_RL_LO && !HEAT_TB_CHAIN
 template <int K, int K1>
 int occ_split_k() {
   int n = 0;

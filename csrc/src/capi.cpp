@@ -281,6 +281,7 @@ void fill_stats(const heat::RunStats& r, heat_run_stats* out) {
   out->checks = r.checks;
   out->resident_passes = r.resident_passes;
   out->resident_giveups = r.resident_giveups;
+  out->chained_passes = r.chained_passes;
 }
 }  // namespace
 

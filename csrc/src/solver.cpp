@@ -140,6 +140,19 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   resident_ = (tile_sized() || resident_sized()) && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
               !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
               (world == 1 || ndev >= local_world || resident_force_);
+  // Chained level-split passes (tb_chain.hip, HEAT_TB_CHAIN=1; off by
+  // default): one-rank GPU runs of the streaming depth-12 pipelines (large
+  // blocks that do not go resident).  Bitwise equal, but 8192^2 ran 3.75 vs
+  // 5.24 Tcells/s: the write-through stores the cross-XCD hand-off needs
+  // cost ~21 %, and passes that drift apart lose the L2 sharing of the
+  // synchronous launches (profiles/r5_chain.md).  Like resident tiles the
+  // chained grid must own its device.
+  chain_ = on_gpu() && world == 1 && !resident_ && T_ == gpu::kTbDeepDepth && tb_kernel() &&
+           sched_ == Schedule::Sync && !staged_ && gpu::tb_tuning().variant < 0 &&
+           env_int("HEAT_TB_CHAIN", 0) != 0;
+  if (env_int("HEAT_TB_TRACE", 0) != 0)
+    std::fprintf(stderr, "[heat solver] rank %d T %d resident %d chain %d sched %d staged %d world %d\n",
+                 tr_->rank(), T_, int(resident_), int(chain_), int(sched_), int(staged_), world);
   if (const char* e = std::getenv("HEAT_TB_RES_GIVEUP"); e && std::strcmp(e, "defer") == 0)
     defer_giveup_ = true;
   // Tests: this rank's first run with resident spans reports a give-up.
@@ -202,8 +215,9 @@ void Solver::alloc() {
     HIP_CHECK(hipHostMalloc(&h_resid_, 256));
     HIP_CHECK(hipMalloc(&d_scratch_, 4096));
     HIP_CHECK(hipMalloc(&d_checksum_, 256));
-    if (resident_) {
-      for (auto& b : xbase_) HIP_CHECK(hipMalloc(&b, size_t(L_.bytes())));
+    if (resident_ || chain_) {
+      if (resident_)
+        for (auto& b : xbase_) HIP_CHECK(hipMalloc(&b, size_t(L_.bytes())));
       // Flags, then the error word and the completion counter: zeroed once
       // here, then by the last tile of every launch (tb_resident.hip).
       HIP_CHECK(hipMalloc(&d_flags_, kResidentFlagBytes + 256));
@@ -962,8 +976,63 @@ void Solver::enqueue_pass(int k, int rl) {
   ++stat_passes_;
 }
 
+int Solver::chain_span(const std::vector<PassPlan>& plan, size_t i) const {
+  if (!chain_ || plan[i].k != T_ || plan[i].rl != 0 || device_users(P_.device >= 0 ? P_.device : 0) > 1)
+    return 0;
+  int n = 0;
+  for (size_t j = i; j < plan.size() && plan[j].k == T_ && plan[j].rl == 0; ++j) ++n;
+  return n;
+}
+
+bool Solver::enqueue_chain(const std::vector<PassPlan>& plan, size_t i0, int n) {
+  const int k = plan[i0].k;
+  TraceRange trace("heat.chain");
+  const int cur0 = cur_;
+  gpu::TbChain ch;
+  ch.passes = n;
+  ch.flags = d_flags_;
+  ch.err = d_flags_ + kResidentFlagBytes / 4;
+  ch.done = ch.err + 1;
+  ch.max_units = int(kResidentFlagBytes / 4);
+  {
+    PhaseScope phase(this, kCompute, s_comp_);
+    const Box own{0, blk_.lx, 0, blk_.ly};
+    gpu::tb_step(field_[cur_], field_[cur_ ^ 1], geom(), &own, 1, k, nullptr, s_comp_,
+                 gpu::tb_tuning().waves, -1, 0, &ch);
+  }
+  if (!ch.chained) {
+    chain_ = false;  // this block's plan does not qualify: one launch per pass from now on
+    return false;
+  }
+  resident_used_ = true;  // the give-up word is read after the run (run_impl)
+  const int out = (n & 1) ? cur0 ^ 1 : cur0;
+  for (int j = 0; j < n; ++j) {
+    PassRec rec;
+    rec.step0 = step_ + int64_t(j) * k;
+    rec.k = k;
+    rec.rl = 0;
+    rec.cur0 = (cur0 + j) & 1;
+    rec.cur1 = (cur0 + j + 1) & 1;
+    rec.gr1 = gr_;
+    rec.gc1 = gc_;
+    pass_log_.push_back(rec);
+  }
+  cur_ = out;
+  step_ += int64_t(n) * k;
+  stat_passes_ += n;
+  stat_chained_ += n;
+  return true;
+}
+
 void Solver::enqueue_segment(const std::vector<PassPlan>& plan) {
   for (size_t i = 0; i < plan.size();) {
+    if (on_gpu()) {
+      const int nc = chain_span(plan, i);
+      if (nc >= 2 && enqueue_chain(plan, i, nc)) {
+        i += size_t(nc);
+        continue;
+      }
+    }
     const int n = on_gpu() ? resident_span(plan, i) : 0;
     if (n >= 2) {
       enqueue_resident(plan, i, n);
@@ -1096,7 +1165,8 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
   const auto key = std::make_tuple(n, phase, cur_, gr_, gc_);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
-    const int64_t p_before = stat_passes_, e_before = stat_exchanges_, r_before = stat_resident_;
+    const int64_t p_before = stat_passes_, e_before = stat_exchanges_, r_before = stat_resident_,
+                  c_before = stat_chained_;
     const bool res_before = resident_used_;
     resident_used_ = false;
     TraceRange trace_capture("heat.capture");
@@ -1127,7 +1197,9 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
     e.exchanges = stat_exchanges_ - e_before;
     e.resident = resident_used_;
     e.resident_passes = stat_resident_ - r_before;
+    e.chained_passes = stat_chained_ - c_before;
     stat_resident_ = r_before;
+    stat_chained_ = c_before;
     resident_used_ = res_before;
     relative(e);
     stat_passes_ = p_before;
@@ -1143,6 +1215,7 @@ void Solver::launch_segment(const std::vector<PassPlan>& plan, int64_t n, int64_
   stat_passes_ += it->second.passes;
   stat_exchanges_ += it->second.exchanges;
   stat_resident_ += it->second.resident_passes;
+  stat_chained_ += it->second.chained_passes;
   *recs = it->second.recs;
   *checks = it->second.checks;
 }
@@ -1400,7 +1473,7 @@ RunStats Solver::run_impl(int64_t steps, bool wait) {
   TraceRange trace("heat.run");
   RunStats s;
   HEAT_CHECK(steps >= 0, "negative step count");
-  const int64_t p0 = stat_passes_, e0 = stat_exchanges_, res0 = stat_resident_;
+  const int64_t p0 = stat_passes_, e0 = stat_exchanges_, res0 = stat_resident_, ch0 = stat_chained_;
   // An enqueued run (enqueue) still in flight: continue its stream; its
   // error word and transport are checked when this call completes.
   const bool cont = pending_;
@@ -1437,6 +1510,7 @@ RunStats Solver::run_impl(int64_t steps, bool wait) {
     s.passes = stat_passes_ - p0;
     s.exchanges = stat_exchanges_ - e0;
     s.resident_passes = stat_resident_ - res0;
+    s.chained_passes = stat_chained_ - ch0;
     return s;
   }
   pending_ = false;
@@ -1470,6 +1544,7 @@ RunStats Solver::run_impl(int64_t steps, bool wait) {
     std::fprintf(stderr, "[heat] rank %d: resident tiles gave up a neighbour wait: this run's "
                          "results are invalid; resident spans off for this solver\n", tr_->rank());
     resident_ = false;
+    chain_ = false;
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second.exec);
     graphs_.clear();
     rccl_graphs_ = false;
@@ -1488,6 +1563,7 @@ RunStats Solver::run_impl(int64_t steps, bool wait) {
   s.passes = stat_passes_ - p0;
   s.exchanges = stat_exchanges_ - e0;
   s.resident_passes = stat_resident_ - res0;
+  s.chained_passes = stat_chained_ - ch0;
   return s;
 }
 

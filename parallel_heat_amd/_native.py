@@ -83,6 +83,7 @@ class HeatRunStats(Structure):
         ("passes", c_int64), ("exchanges", c_int64), ("checks", c_int64),
         ("t_exchange", c_double), ("t_compute", c_double), ("t_reduce", c_double),
         ("resident_passes", c_int64), ("resident_giveups", c_int64),
+        ("chained_passes", c_int64),
     ]
 
 

@@ -43,6 +43,9 @@ class RunResult:
     # 1: a resident launch gave up a neighbour wait (results invalid); only
     # returned with HEAT_TB_RES_GIVEUP=defer, otherwise run() raises.
     resident_giveups: int = 0
+    # passes run inside chained level-split launches (one-rank runs of the
+    # streaming depth-12 pipelines, no grid-wide boundary between passes)
+    chained_passes: int = 0
 
     @property
     def mcells_per_s(self) -> float:
@@ -196,7 +199,7 @@ class HeatSolver:
         return RunResult(st.steps_done, st.total_steps, bool(st.converged), st.converged_at,
                          st.last_resid, st.seconds, st.passes, st.exchanges, st.checks,
                          self.config.nx * self.config.ny, st.t_exchange, st.t_compute,
-                         st.t_reduce, st.resident_passes, st.resident_giveups)
+                         st.t_reduce, st.resident_passes, st.resident_giveups, st.chained_passes)
 
     def time_exchange(self, depth: int, iters: int = 20) -> tuple:
         """(seconds per grouped halo exchange of `depth` rows/columns on this

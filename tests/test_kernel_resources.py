@@ -30,7 +30,7 @@ LIB = os.path.join(ROOT, "parallel_heat_amd", "_lib", "libheat.so")
 BUDGET = os.path.join(ROOT, "tests", "data", "kernel_scratch_budget.json")
 
 # Namespaces of the hot kernel families (tbp / tbn: diagnostic variants).
-HOT = re.compile(r"^_ZN4heat3gpu(3tbx|4tbxm|4tbxn|3tbs|3tbw)")
+HOT = re.compile(r"^_ZN4heat3gpu(3tbx|4tbxm|4tbxn|3tbc|3tbs|3tbw)")
 # Must be spill-free: the tile passes (with or without residuals, since
 # round 5's branch-free last-step stores), default (mixed) lane shifts XL 2.
 # Exempt: 20 x 16 RES 1 (12 B/lane).  The unchecked resident launches may

@@ -95,7 +95,7 @@ def main():
     a = ap.parse_args()
     ks = kernels(a.lib)
     if a.budget:
-        hot = re.compile(r"^_ZN4heat3gpu(3tbx|4tbxm|4tbxn|3tbs|3tbw)")
+        hot = re.compile(r"^_ZN4heat3gpu(3tbx|4tbxm|4tbxn|3tbc|3tbs|3tbw)")
         print(json.dumps({k["name"]: k["scratch"] for k in sorted(ks, key=lambda k: k["name"])
                           if hot.match(k["name"]) and k["scratch"] > 0}, indent=1))
         return 0
