@@ -795,8 +795,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     const int G = (args.flags & tbdetail::kTbAgePairs) ? args.age_groups : 1;
     int blocks = (args.total_waves + 1) / 2;
     if (G > 1) blocks = (blocks + 7) / 8 * 8 * G;
-    static int occ = -1;  // one device model per process (gfx950)
-    if (occ < 0) occ = tbc::occupancy_chain(kTbDeepDepth);
+    static const int occ = tbc::occupancy_chain(kTbDeepDepth);  // one device model (gfx950)
     int dev = 0, cus = 0;
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));

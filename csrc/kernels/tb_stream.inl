@@ -1081,14 +1081,17 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_ch
       src = dst;
       dst = const_cast<float*>(t);
     }
-    if (stage == 1 && lane == 0) {
+    if (stage == 1) {
       // Every other unit is past its last poll once the counter reaches
-      // nunits: the last one re-zeroes the flags for the next launch.
-      const unsigned n = __hip_atomic_fetch_add(c.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      // nunits: the last one re-zeroes the flags (all 64 lanes) and the
+      // counter for the next launch.
+      unsigned n = 0;
+      if (lane == 0) n = __hip_atomic_fetch_add(c.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      n = __builtin_amdgcn_readfirstlane(n);
       if (n + 1 == nunits) {
-        for (unsigned i = 0; i < nunits; ++i)
+        for (unsigned i = unsigned(lane); i < nunits; i += 64)
           __hip_atomic_store(c.flags + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(c.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
