@@ -9,6 +9,11 @@
 #define HEAT_TB_PACKED 0
 #define HEAT_TB_SPLIT 1
 #define HEAT_TB_BPERMUTE 1
+// Streaming rows (non-temporal loads / stores, as tb_split_nt.hip): checked
+// runs every 20 steps +0.8 % at 8192^2, +0.5 % on the 2-GPU plate
+// (profiles/r5_stores.md).
+#define HEAT_TB_NTSTORE 1
+#define HEAT_TB_NTLOAD 1
 #define HEAT_TB_SPLIT_RL_LO 1
 #define HEAT_TB_SPLIT_RL_HI 4
 #define HEAT_TB_SPLIT_RL_FN launch_split_rl_a
