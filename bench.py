@@ -55,9 +55,12 @@ watchdog ends a hung run with a stack dump instead of letting it hang
 (`--watchdog-s`).
 
 Exchange model (multi-GPU): before pruning autotune candidates, grouped halo
-exchanges of the first candidate are timed at two depths on the real ranks;
-the fitted latency and per-link GB/s replace the stated constants of
-parallel/model.py in the pruning and in "predicted" / "model".
+exchanges of the first candidate are timed at three depths (5 samples of 20
+exchanges each) on the real ranks; a fit with a positive slope and R^2 >= 0.8
+over the per-size medians replaces the stated latency and per-link GB/s of
+parallel/model.py in the pruning and in "predicted" / "model"; a fit that
+fails those checks (model.xgmi.fit_ok false) prunes nothing.  The pruning
+always keeps the best-predicted candidate of every (layout, halo passes).
 """
 from __future__ import annotations
 
@@ -250,7 +253,7 @@ def main() -> int:
         # block shape: time each on the real ranks before the timed region.
         from parallel_heat_amd.parallel.model import fit_exchange, predict, prune
         from parallel_heat_amd.parallel.tune import (autotune, default_candidates, describe,
-                                                     measure_exchange)
+                                                     exchange_depths, measure_exchange)
 
         watchdog("autotune", args.watchdog_s)
         all_cands = default_candidates(cfg, world,
@@ -261,7 +264,7 @@ def main() -> int:
         # (grouped exchanges of the first candidate's messages at two depths)
         # before they prune anything.
         xgmi = exchange_probe(all_cands[0], info, shared, world, HeatSolver, measure_exchange,
-                              fit_exchange, rank)
+                              exchange_depths, fit_exchange, rank)
         cands = prune(all_cands, world, xgmi=xgmi)
         pruned = [dict(describe(c, world),
                        predicted_ms_per_1000=predict(c, world, xgmi=xgmi)["ms_per_1000"])
@@ -436,11 +439,13 @@ def main() -> int:
     return 0 if verified is not False else 2
 
 
-def exchange_probe(cfg, info, shared, world, HeatSolver, measure_exchange, fit_exchange, rank):
+def exchange_probe(cfg, info, shared, world, HeatSolver, measure_exchange, exchange_depths,
+                   fit_exchange, rank):
     """Measured exchange parameters (latency, GB/s per link) from grouped halo
-    exchanges of cfg's layout at its full halo depth and a quarter of it, max
-    over the ranks (collective); None (the stated model) if the probe fails
-    on any rank."""
+    exchanges of cfg's layout at three depths (H, H/2, H/4), 5 interleaved
+    samples of 20 exchanges each, max over the ranks (collective); the fit
+    takes medians and says whether it may prune (fit_ok).  None (the stated
+    model) if the probe fails on any rank."""
     pts = None
     try:
         with HeatSolver(cfg, dist_info=info, shared=shared) as s:
@@ -449,7 +454,7 @@ def exchange_probe(cfg, info, shared, world, HeatSolver, measure_exchange, fit_e
                 t = torch.tensor([x], dtype=torch.float64, device="cuda")
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 return float(t.item())
-            pts = measure_exchange(s, sorted({H, max(1, H // 4)}), iters=10, agree_max=agree_max)
+            pts = measure_exchange(s, exchange_depths(H), iters=20, reps=5, agree_max=agree_max)
     except Exception as e:  # noqa: BLE001 - diagnostics; the stated model stays
         log(rank, f"exchange probe failed ({e})")
     ok = torch.tensor([1 if pts else 0], dtype=torch.int32, device="cuda")

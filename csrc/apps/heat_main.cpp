@@ -21,6 +21,7 @@
 
 #include "heat/capi.h"
 #include "heat/common.hpp"
+#include "heat/plan.hpp"
 #include "heat/io.hpp"
 #include "heat/solver.hpp"
 
@@ -345,7 +346,21 @@ int main(int argc, char** argv) {
     const int ranks = std::max(gpus, env_i("WORLD_SIZE", 1));
     const Cart cart(ranks, P.decomp, P.px, P.py, P.nx, P.ny);
     const int depth = P.tb_depth > 0 ? P.tb_depth : 12;
-    const int m = ranks > 1 ? (P.halo_passes > 0 ? P.halo_passes : 8) : 1;
+    // Passes per exchange as the solver picks them (resident-aware unless
+    // --halo-passes is given; resident_halo_passes), with the host-side
+    // gfx950 resident fit: whether every rank's span box runs as one-round
+    // resident tiles.
+    auto fits = [&](const Box& b) { return resident_fits_static(b, depth); };
+    int m = 1;
+    if (ranks > 1) {
+      const int rm = resident_halo_passes(cart, P.nx, P.ny, depth, 8, fits);
+      m = P.halo_passes > 0 ? P.halo_passes : rm >= kResMinPasses ? rm : 8;
+    }
+    bool resident = true;
+    for (int r = 0; r < ranks; ++r) {
+      const Block b = make_block(cart, r, P.nx, P.ny);
+      resident = resident && fits(ranks > 1 ? span_box(cart, b, depth, m) : Box{0, b.lx, 0, b.ly});
+    }
     int64_t worst = 0, worst_rank = 0;
     for (int r = 0; r < ranks; ++r) {
       const Block b = make_block(cart, r, P.nx, P.ny);
@@ -364,9 +379,11 @@ int main(int argc, char** argv) {
     }
     std::printf("{\"nx\": %lld, \"ny\": %lld, \"ranks\": %d, \"process_grid\": \"%dx%d\", "
                 "\"bytes_per_gpu\": %lld, \"gb_per_gpu\": %.3f, \"worst_rank\": %lld, "
-                "\"fits_288gb\": %s}\n",
+                "\"fits_288gb\": %s, \"tb_depth\": %d, \"halo_passes\": %d, \"halo\": %d, "
+                "\"resident\": %s}\n",
                 (long long)P.nx, (long long)P.ny, ranks, cart.px, cart.py, (long long)worst,
-                double(worst) / 1e9, (long long)worst_rank, worst < int64_t(288e9 * 0.95) ? "true" : "false");
+                double(worst) / 1e9, (long long)worst_rank, worst < int64_t(288e9 * 0.95) ? "true" : "false",
+                depth, m, depth * m, resident ? "true" : "false");
     return 0;
   }
   const int world = env_i("WORLD_SIZE", 1), rank = env_i("RANK", 0);
@@ -434,9 +451,11 @@ int main(int argc, char** argv) {
                         : make_loopback_transport(hub, r, Pr.device),
                    &reg);
         } catch (const std::exception& e) {
-          errors[r] = e.what();
           {
+            // Under the lock: the main thread reads errors[] on the
+            // grace-timeout path while other ranks may still be unwinding.
             std::lock_guard<std::mutex> lk(done_mu);
+            errors[r] = e.what();
             failed = true;
           }
           // Loopback peers blocked on this rank's messages throw in turn;

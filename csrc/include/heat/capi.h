@@ -118,6 +118,9 @@ int heat_solver_run(heat_solver* s, int64_t steps, heat_run_stats* out);
 int heat_solver_enqueue(heat_solver* s, int64_t steps, heat_run_stats* out);
 /* RCCL on one rank: self send/recv (eager or hipGraph-captured) + all-reduce. */
 int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double* gbps);
+/* RCCL abort while another thread issues calls on the communicator (one-rank
+   communicators, `rounds` rounds); *calls = calls completed before the aborts. */
+int heat_rccl_abort_race_test(int device, int rounds, int* calls);
 /* Loopback transport: ranks are threads of this process sharing one hub. */
 int heat_loopback_hub_create(int world, void** out);
 int heat_loopback_hub_destroy(void* hub);

@@ -35,6 +35,7 @@
 #include <utility>
 #include <vector>
 
+#include "heat/common.hpp"
 #include "heat/io.hpp"
 #include "heat/kernels.hpp"
 #include "heat/params.hpp"
@@ -42,6 +43,14 @@
 #include "heat/transport.hpp"
 
 namespace heat {
+
+// A run-time error every rank meets at the same point, decided from
+// all-reduced or global quantities (a non-finite all-reduced residual): after
+// it a rank's queued exchanges were all matched, so the communicator may be
+// kept (Solver::run_guarded's "[clean]").  Any other error aborts it.
+struct GlobalError : Error {
+  using Error::Error;
+};
 
 struct RunStats {
   int64_t steps_done = 0;     // steps advanced by this call
@@ -182,6 +191,7 @@ class Solver {
   // the last pass (device-judged runs), and every tile of the first pass's
   // box co-resident.
   int resident_span(const std::vector<PassPlan>& plan, size_t i) const;
+  int res_span_max_ = 0;  // HEAT_TB_RES_SPAN (diagnostics; 0: no cap)
   static int device_users(int dev);  // live GPU solvers of this process on dev
   void enqueue_resident(const std::vector<PassPlan>& plan, size_t i0, int n);
   // Chained passes (one-rank runs of the streaming level-split build): the

@@ -103,6 +103,10 @@ void rccl_unique_id(void* out128);
 // Single-rank RCCL check on `device`: self send/recv of `bytes` (eager or in
 // a captured hipGraph) and an all-reduce; throws on wrong data, returns GB/s.
 double rccl_self_test(int device, size_t bytes, bool graph, int iters);
+// Abort while another thread issues RCCL calls, `rounds` times on a one-rank
+// communicator; throws unless every round ends with the caller's calls
+// refused ("aborted").  Returns the calls completed before the aborts.
+int rccl_abort_race_test(int device, int rounds);
 
 // TCP: rank 0 listens on (addr, port); everyone connects to everyone
 // (full mesh, one socket per peer pair).

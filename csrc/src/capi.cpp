@@ -187,6 +187,10 @@ int heat_rccl_self_test(int device, int64_t bytes, int graph, int iters, double*
   return guard([&] { *gbps = heat::rccl_self_test(device, size_t(bytes), graph != 0, iters); });
 }
 
+int heat_rccl_abort_race_test(int device, int rounds, int* calls) {
+  return guard([&] { *calls = heat::rccl_abort_race_test(device, rounds); });
+}
+
 int heat_loopback_hub_create(int world, void** out) {
   return guard([&] { *out = heat::loopback_hub_create(world); });
 }

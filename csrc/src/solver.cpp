@@ -13,6 +13,7 @@
 #include "heat/common.hpp"
 #include "heat/cpu_backend.hpp"
 #include "heat/kernels.hpp"
+#include "heat/plan.hpp"
 #include "heat/trace.hpp"
 
 namespace heat {
@@ -92,28 +93,6 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   sched_ = P_.schedule == Schedule::Auto ? Schedule::Sync : P_.schedule;
   if (!tb_kernel() || world == 1 || !P_.overlap)
     sched_ = Schedule::Sync;
-  // Ghost depth H = m*T: with the Sync schedule one exchange feeds m passes,
-  // each computing the still-valid part of the ghost ring redundantly.
-  int m = 1;
-  if (sched_ == Schedule::Sync && world > 1) {
-    // m = 8 (H = 64 rows at K = 8, 96 at K = 12): larger m trades a few
-    // percent of redundant ghost compute for fewer exchanges, whose
-    // latency dominates on small blocks (profiles/halo_passes_r1.md).
-    m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 8) : 1);
-    m = int(std::max<int64_t>(1, std::min<int64_t>(m, min_ext / T_)));
-  }
-  H_ = m * T_;
-  // A rank must own at least H rows/columns along every decomposed axis so
-  // that an H-deep halo comes from its direct neighbour only.
-  HEAT_CHECK(cart_.px == 1 || blk_.lx >= H_, "block of %lld rows is thinner than halo depth %d",
-             (long long)blk_.lx, H_);
-  HEAT_CHECK(cart_.py == 1 || blk_.ly >= H_, "block of %lld cols is thinner than halo depth %d",
-             (long long)blk_.ly, H_);
-  // The boundary-first pipeline needs an interior box off H-deep bands.
-  if (sched_ == Schedule::Pipeline &&
-      !(min_lx > 2 * int64_t(H_) && round_down(min_ly - H_, 4) > round_up(H_, 4)))
-    sched_ = Schedule::Sync;
-  L_ = Layout::make(blk_.lx, blk_.ly, H_);
   staged_ = on_gpu() && !tr_->device_memory() && world > 1;
   // Resident tiles for the workgroup-tile shapes (small per-rank blocks):
   // even depths, the synchronous schedule, the automatic variant choice;
@@ -129,17 +108,63 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   // (LOCAL_WORLD_SIZE under torchrun; the whole world otherwise), so a
   // multi-node run with a GPU per local rank still goes resident.
   int ndev = 0;
-  if (on_gpu() && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  if (on_gpu()) {
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    HIP_CHECK(hipSetDevice(P_.device >= 0 ? P_.device : 0));  // occupancy queries below
+  }
   const int local_world = std::min(world, std::max(1, env_int("LOCAL_WORLD_SIZE", world)));
   const int res_env = env_int("HEAT_TB_RESIDENT", 1);
   resident_force_ = res_env == 2;
+  // Diagnostics: at most this many passes per resident span (a one-GPU
+  // plate timed at the span length of an m-pass exchange interval).
+  res_span_max_ = env_int("HEAT_TB_RES_SPAN", 0);
+  const bool res_ok = on_gpu() && tb_kernel() && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
+                      !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
+                      (world == 1 || ndev >= local_world || resident_force_);
+  // Ghost depth H = m*T: with the Sync schedule one exchange feeds m passes,
+  // each computing the still-valid part of the ghost ring redundantly.
+  int m = 1;
+  if (sched_ == Schedule::Sync && world > 1) {
+    // m = 8 (H = 64 rows at K = 8, 96 at K = 12): larger m trades a few
+    // percent of redundant ghost compute for fewer exchanges, whose
+    // latency dominates on small blocks (profiles/halo_passes_r1.md).
+    // Unless set, m is resident-aware: when the owned blocks have a
+    // one-round resident plan, the largest m <= 8 whose span boxes still
+    // have one (8192^2 on 2 x 2 ranks: m = 5, 4144-cell boxes in 20 x 16
+    // tiles, instead of m = 8 whose 4180-cell boxes ran the split
+    // pipelines at 3.9 Tcells/s per rank; resident_halo_passes).
+    // A span of m passes pays one whole-tile load and store (what a per-pass
+    // tile launch pays every pass), so short spans lose their edge: below
+    // kResMinPasses the split pipelines at m = 8 are kept.
+    m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 0) : 1);
+    if (m <= 0) {
+      m = 8;
+      if (res_ok) {
+        const int rm = resident_halo_passes(cart_, P_.nx, P_.ny, T_, 8, [&](const Box& b) {
+          return gpu::tb_resident_fits(b, T_);
+        });
+        if (rm >= kResMinPasses) m = rm;
+      }
+    }
+    m = int(std::max<int64_t>(1, std::min<int64_t>(m, min_ext / T_)));
+  }
+  H_ = m * T_;
+  // A rank must own at least H rows/columns along every decomposed axis so
+  // that an H-deep halo comes from its direct neighbour only.
+  HEAT_CHECK(cart_.px == 1 || blk_.lx >= H_, "block of %lld rows is thinner than halo depth %d",
+             (long long)blk_.lx, H_);
+  HEAT_CHECK(cart_.py == 1 || blk_.ly >= H_, "block of %lld cols is thinner than halo depth %d",
+             (long long)blk_.ly, H_);
+  // The boundary-first pipeline needs an interior box off H-deep bands.
+  if (sched_ == Schedule::Pipeline &&
+      !(min_lx > 2 * int64_t(H_) && round_down(min_ly - H_, 4) > round_up(H_, 4)))
+    sched_ = Schedule::Sync;
+  L_ = Layout::make(blk_.lx, blk_.ly, H_);
   // Blocks past the tile threshold whose resident grid still fits one
   // dispatch round (the 4-GPU blocks 2048 x 8192 / 4096 x 4096: 20 x 16
   // tiles) go resident too; other large blocks never allocate the exchange
   // fields (two more fields' worth of memory).
-  resident_ = (tile_sized() || resident_sized()) && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
-              !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
-              (world == 1 || ndev >= local_world || resident_force_);
+  resident_ = res_ok && (tile_sized() || resident_sized());
   // Chained level-split passes (tb_chain.hip, HEAT_TB_CHAIN=1; off by
   // default): one-rank GPU runs of the streaming depth-12 pipelines (large
   // blocks that do not go resident).  Bitwise equal, but 8192^2 ran 3.75 vs
@@ -717,6 +742,7 @@ int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
         (!gated() || plan[j].rl % 2 != 0 || nchk == gpu::kTbResidentMaxChecks))
       break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
+    if (n == res_span_max_) break;
     if (ns) gr -= k;
     if (ew) gc = round_down(gc - k, 4);
     ++n;
@@ -1252,8 +1278,8 @@ void Solver::run_segments(int64_t steps, RunStats& s) {
       ++s.checks;
       s.last_resid = r;
       if (!(r == r) || std::isinf(r))
-        throw_error(__FILE__, __LINE__,
-                    strprintf("non-finite residual (%g) at step %lld", double(r), (long long)step_));
+        throw GlobalError(strprintf("solver.cpp:%d: non-finite residual (%g) at step %lld", __LINE__,
+                                    double(r), (long long)step_));
       if (converged_value(r)) {
         s.converged = true;
         s.converged_at = step_;
@@ -1344,9 +1370,8 @@ void Solver::run_gated(int64_t steps, RunStats& s) {
   step_ = c;
   s.steps_done = c - step0;
   if (gate.reason == 2)
-    throw_error(__FILE__, __LINE__,
-                strprintf("non-finite residual (%g) at step %lld", double(s.last_resid),
-                          (long long)c));
+    throw GlobalError(strprintf("solver.cpp:%d: non-finite residual (%g) at step %lld", __LINE__,
+                                double(s.last_resid), (long long)c));
   s.converged = true;
   s.converged_at = c;
 }
@@ -1410,16 +1435,18 @@ RunStats Solver::run_guarded(int64_t steps, bool wait) {
         if (g) (void)hipGraphDestroy(g);
         capturing_ = false;
       }
-      // A failure after which this rank's queued work still completes (every
-      // exchange and all-reduce it enqueued was matched, no transport error):
-      // a planning check or a non-finite residual, which every rank meets at
-      // the same point since those decisions are global.  The communicator
-      // stays usable; the message says so ("[clean]"), so a caller that
-      // agrees with its peers (parallel.tune.autotune) can go on.  Anything
-      // else aborts it so that peers waiting on this rank fail instead of
-      // hanging.
+      // A failure of a class every rank meets at the same point (GlobalError:
+      // a non-finite all-reduced residual) after which this rank's queued
+      // work still completes (every exchange and all-reduce it enqueued was
+      // matched, no transport error).  The communicator stays usable; the
+      // message says so ("[clean]"), so a caller that agrees with its peers
+      // (parallel.tune.autotune) can go on.  Anything else -- a rank-local
+      // check included, which may have thrown before an exchange its peers
+      // posted -- aborts it so that peers waiting on this rank fail instead
+      // of hanging.
       bool clean = false;
-      if (on_gpu() && !aborted_.load() && !staged_failed_.load()) {
+      if (dynamic_cast<const GlobalError*>(&e) != nullptr && on_gpu() && !aborted_.load() &&
+          !staged_failed_.load()) {
         try {
           sync_watch();
           tr_->check();

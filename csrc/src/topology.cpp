@@ -1,4 +1,5 @@
 // Process topology / decomposition (see topology.hpp for the reference map).
+#include "heat/plan.hpp"
 #include "heat/topology.hpp"
 
 #include <algorithm>
@@ -122,6 +123,50 @@ Layout Layout::make(int64_t lx, int64_t ly, int halo) {
   L.pitch = round_up(L.hy + ly + L.hy + 256, 64);
   L.rows = lx + 2 * int64_t(halo);
   return L;
+}
+
+Box span_box(const Cart& cart, const Block& b, int depth, int m) {
+  const int64_t gr = cart.px > 1 ? int64_t(m - 1) * depth : 0;
+  const int64_t gc = cart.py > 1 ? round_down(int64_t(m - 1) * depth, 4) : 0;
+  return Box{b.nbr[North] >= 0 ? -gr : 0, b.lx + (b.nbr[South] >= 0 ? gr : 0),
+             b.nbr[West] >= 0 ? -gc : 0, b.ly + (b.nbr[East] >= 0 ? gc : 0)};
+}
+
+int resident_halo_passes(const Cart& cart, int64_t nx, int64_t ny, int depth, int mmax,
+                         const std::function<bool(const Box&)>& fits) {
+  if (cart.world < 2 || depth < 1) return 0;
+  std::vector<Block> blocks;
+  int64_t min_ext = INT64_MAX;
+  for (int r = 0; r < cart.world; ++r) {
+    blocks.push_back(make_block(cart, r, nx, ny));
+    const Block& b = blocks.back();
+    if (!fits(Box{0, b.lx, 0, b.ly})) return 0;
+    if (cart.px > 1) min_ext = std::min(min_ext, b.lx);
+    if (cart.py > 1) min_ext = std::min(min_ext, b.ly);
+  }
+  for (int m = int(std::min<int64_t>(mmax, min_ext / depth)); m >= 2; --m) {
+    bool ok = true;
+    for (const Block& b : blocks) ok = ok && fits(span_box(cart, b, depth, m));
+    if (ok) return m;
+  }
+  return 0;
+}
+
+bool resident_fits_static(const Box& box, int depth, int cus) {
+  // (rows per wave, waves per workgroup, workgroups per CU).
+  static constexpr int kShapes[][3] = {{12, 8, 2}, {13, 8, 2}, {14, 8, 2}, {16, 8, 2},
+                                       {20, 8, 1}, {24, 8, 1}, {12, 16, 1}, {20, 16, 1}};
+  if (box.empty() || depth < 4 || depth % 2 != 0 || box.c0 % 4 != 0) return false;
+  const int64_t W = 256 - 2 * round_up(int64_t(depth), 4);
+  for (const auto& s : kShapes) {
+    const int64_t hmax = int64_t(s[0]) * s[1] - 2 * int64_t(depth);
+    if (hmax < std::max(depth, 4)) continue;
+    const int64_t chunks = ceil_div(box.rows(), hmax);
+    if (ceil_div(box.cols(), W) * chunks <= int64_t(cus) * s[2] &&
+        ceil_div(box.rows(), chunks) >= depth)
+      return true;
+  }
+  return false;
 }
 
 }  // namespace heat

@@ -12,7 +12,9 @@
 #include <algorithm>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "heat/common.hpp"
@@ -51,12 +53,17 @@ class RcclTransport final : public Transport {
   bool device_memory() const override { return true; }
   bool graph_capturable() const override { return true; }
 
-  // Every call holds mu_: abort() may come from another thread (a failing
-  // rank of a single-process group, or a solver's watchdog) and frees comm_.
+  // Every call holds mu_ (calls are serialised) and is a Call: it announces
+  // itself in inflight_, then re-checks aborted_ before touching comm_.
+  // abort() may come from another thread (a failing rank of a
+  // single-process group, or a solver's watchdog) and frees comm_ in
+  // ncclCommAbort; it sets aborted_ first, then looks at inflight_ (both
+  // sequentially consistent: either the call sees aborted_ and throws
+  // without using comm_, or abort sees the call), so no call STARTS on a
+  // freed communicator.
   void sendrecv(const Msg* msgs, int n, hipStream_t st) override {
     if (n == 0) return;
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < n; ++i) {
       const Msg& m = msgs[i];
@@ -66,18 +73,15 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max(float* buf, int count, hipStream_t st) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat, ncclMax, comm_, st));
   }
   void allreduce_sum_f64(double* buf, int count, hipStream_t st) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclFloat64, ncclSum, comm_, st));
   }
   void allreduce_sum_u64(uint64_t* buf, int count, hipStream_t st) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     NCCL_CHECK(ncclAllReduce(buf, buf, size_t(count), ncclUint64, ncclSum, comm_, st));
   }
   void barrier() override {
@@ -86,16 +90,14 @@ class RcclTransport final : public Transport {
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      live();
+      Call c(*this);
       NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclFloat, ncclMax, comm_, st));
     }
     HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipStreamDestroy(st));
   }
   void check() override {
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     ncclResult_t async = ncclSuccess;
     NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
     if (async != ncclSuccess && async != ncclInProgress)
@@ -106,16 +108,20 @@ class RcclTransport final : public Transport {
   // that will never answer; later calls throw.  Idempotent.  Not under mu_:
   // a peer thread of a single-process group can hold it while blocked in
   // ncclGroupEnd waiting for the dead rank, and the abort is what unblocks
-  // it (ncclCommAbort is meant to be called from another thread).  comm_
-  // keeps its value; the flag turns every later call away (live()).
+  // it (ncclCommAbort is meant to be called from another thread).  Calls
+  // already inside RCCL get kAbortGraceMs to leave; one still inside then is
+  // blocked in its LAST RCCL call (ncclGroupEnd / ncclAllReduce: the enqueue
+  // calls before them do not wait on peers), which the abort ends with an
+  // error, so it issues no further call on the freed communicator.
   void abort() override {
     if (aborted_.exchange(true)) return;
+    for (int i = 0; i < kAbortGraceMs && inflight_.load() > 0; ++i)
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
     if (comm_) (void)ncclCommAbort(comm_);
   }
   const char* name() const override { return "rccl"; }
   TransportInfo info() const override {
-    std::lock_guard<std::mutex> lk(mu_);
-    live();
+    Call c(*this);
     TransportInfo t;
     NCCL_CHECK(ncclCommCount(comm_, &t.nranks));
     NCCL_CHECK(ncclCommCuDevice(comm_, &t.device));
@@ -126,11 +132,23 @@ class RcclTransport final : public Transport {
   }
 
  private:
-  void live() const {
-    if (!comm_ || aborted_.load()) throw_error(__FILE__, __LINE__, "RCCL communicator was aborted");
-  }
+  static constexpr int kAbortGraceMs = 200;
+  // One RCCL call: mu_ held, announced in inflight_, aborted_ re-checked.
+  struct Call {
+    const RcclTransport& t;
+    std::lock_guard<std::mutex> lk;
+    explicit Call(const RcclTransport& tr) : t(tr), lk(tr.mu_) {
+      t.inflight_.fetch_add(1);
+      if (!t.comm_ || t.aborted_.load()) {
+        t.inflight_.fetch_sub(1);
+        throw_error(__FILE__, __LINE__, "RCCL communicator was aborted");
+      }
+    }
+    ~Call() { t.inflight_.fetch_sub(1); }
+  };
   int rank_, world_;
   mutable std::mutex mu_;
+  mutable std::atomic<int> inflight_{0};
   std::atomic<bool> abandoned_{false}, aborted_{false};
   ncclComm_t comm_ = nullptr;
   float* scratch_ = nullptr;
@@ -205,6 +223,55 @@ double rccl_self_test(int device, size_t bytes, bool graph, int iters) {
   HEAT_CHECK(ok, "RCCL self send/recv delivered wrong bytes");
   HEAT_CHECK(ok_ar, "RCCL all-reduce on one rank changed the data");
   return double(bytes) * iters / (double(ms) * 1e-3) / 1e9;
+}
+
+int rccl_abort_race_test(int device, int rounds) {
+  // abort() used to free the communicator while another thread
+  // could be between its live() check and its next RCCL call.  Each round:
+  // a one-rank communicator, a thread issuing self send/recv and all-reduces
+  // back to back, an abort from this thread while it runs.  The caller
+  // thread must end with "aborted" errors only (no crash, no hang); returns
+  // the calls the worker completed over all rounds.
+  HIP_CHECK(hipSetDevice(device));
+  float* buf = nullptr;
+  HIP_CHECK(hipMalloc(&buf, 1 << 16));
+  hipStream_t st;
+  HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  int done_calls = 0;
+  for (int r = 0; r < rounds; ++r) {
+    unsigned char uid[128];
+    rccl_unique_id(uid);
+    auto tr = make_rccl_transport(0, 1, uid, device);
+    std::atomic<bool> started{false};
+    std::string err;
+    int calls = 0;
+    std::thread worker([&] {
+      (void)hipSetDevice(device);
+      Msg m{0, buf, 4096, buf + 4096, 4096};
+      try {
+        for (;;) {
+          tr->sendrecv(&m, 1, st);
+          tr->allreduce_max(buf + 8192, 16, st);
+          ++calls;
+          started = true;
+        }
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+    });
+    while (!started.load()) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    std::this_thread::sleep_for(std::chrono::microseconds(200 * (r % 5)));
+    tr->abort();
+    worker.join();
+    (void)hipStreamSynchronize(st);  // an aborted communicator's kernels end with errors
+    (void)hipGetLastError();
+    HEAT_CHECK(err.find("aborted") != std::string::npos || err.find("RCCL") != std::string::npos,
+               "round %d: worker ended with '%s'", r, err.c_str());
+    done_calls += calls;
+  }
+  (void)hipStreamDestroy(st);
+  (void)hipFree(buf);
+  return done_calls;
 }
 
 void rccl_unique_id(void* out128) {

@@ -133,6 +133,7 @@ _SIGS = {
     "heat_solver_enqueue": (c_int, [c_void_p, c_int64, POINTER(HeatRunStats)]),
     "heat_loopback_hub_create": (c_int, [c_int, POINTER(c_void_p)]),
     "heat_rccl_self_test": (c_int, [c_int, c_int64, c_int, c_int, POINTER(c_double)]),
+    "heat_rccl_abort_race_test": (c_int, [c_int, c_int, POINTER(c_int)]),
     "heat_loopback_hub_destroy": (c_int, [c_void_p]),
     "heat_loopback_hub_fail": (c_int, [c_void_p]),
     "heat_solver_reset": (c_int, [c_void_p]),

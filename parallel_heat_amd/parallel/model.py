@@ -80,12 +80,50 @@ RES_SHAPES = [(12, 8, 2), (13, 8, 2), (14, 8, 2), (16, 8, 2), (20, 8, 1), (24, 8
 
 def resident_fits(rows: int, cols: int, depth: int = 12) -> bool:
     """A rows x cols box has a one-round resident plan (all tiles co-resident)."""
-    strips = math.ceil(cols / STRIP_COLS)
+    strips = math.ceil(cols / (256 - 2 * ((depth + 3) // 4 * 4)))
     for r, nw, occ in RES_SHAPES:
         h = r * nw - 2 * depth
-        if h >= depth and strips * math.ceil(rows / h) <= CUS * occ:
+        if h < max(depth, 4):
+            continue
+        chunks = math.ceil(rows / h)
+        if strips * chunks <= CUS * occ and math.ceil(rows / chunks) >= depth:
             return True
     return False
+
+
+RES_MIN_PASSES = 4  # csrc/include/heat/plan.hpp kResMinPasses
+
+
+def _blocks(n: int, parts: int) -> List[int]:
+    """Remainder-aware 1-D block sizes (topology.cpp block_span)."""
+    return [n // parts + (1 if i < n % parts else 0) for i in range(parts)]
+
+
+def resident_halo_passes(nx: int, ny: int, px: int, py: int, depth: int = 12,
+                         mmax: int = 8) -> int:
+    """The solver's resident-aware passes per exchange (topology.cpp
+    resident_halo_passes): the largest m in [2, mmax] for which every rank's
+    first span box -- the owned block grown by (m - 1) * depth on each side
+    with a neighbour -- has a one-round resident plan; 0 if the owned blocks
+    have none or no m does.  The solver keeps m = 8 below RES_MIN_PASSES."""
+    if px * py < 2:
+        return 0
+    rows, cols = _blocks(nx, px), _blocks(ny, py)
+    if not all(resident_fits(r, c, depth) for r in rows for c in cols):
+        return 0
+    ext = min((rows if px > 1 else []) + (cols if py > 1 else []))
+    for m in range(min(mmax, ext // depth), 1, -1):
+        gr = (m - 1) * depth if px > 1 else 0
+        gc = ((m - 1) * depth) // 4 * 4 if py > 1 else 0
+        ok = True
+        for i, r in enumerate(rows):
+            for j, c in enumerate(cols):
+                er = gr * ((i > 0) + (i < px - 1))
+                ec = gc * ((j > 0) + (j < py - 1))
+                ok = ok and resident_fits(r + er, c + ec, depth)
+        if ok:
+            return m
+    return 0
 
 
 def _interp(pts, srps: float) -> float:
@@ -116,30 +154,61 @@ def _grid(cfg: HeatConfig, world: int) -> tuple:
     return d[0], d[1]
 
 
+# A fit is trusted (and may prune autotune candidates) only with at least
+# FIT_MIN_SIZES distinct message sizes, a positive slope and an R^2 of at
+# least FIT_MIN_R2 over the per-size medians.
+FIT_MIN_SIZES = 3
+FIT_MIN_R2 = 0.8
+
+
 def fit_exchange(points: Sequence[tuple], base: Dict = None) -> Dict:
     """Exchange parameters from measured (message bytes, seconds per grouped
-    exchange) points on the real ranks (``HeatSolver.time_exchange``, max over
-    ranks): latency = intercept, link_gbps = 1 / slope of a least-squares line
-    (one point: the stated bandwidth, latency = the rest).  Returns a copy of
-    `base` (default XGMI) with those two replaced and the points attached."""
+    exchange) samples on the real ranks (``HeatSolver.time_exchange``, max
+    over ranks; several samples per size allowed): the median per size, then
+    latency = intercept and link_gbps = 1 / slope of a least-squares line.
+
+    Returns a copy of `base` (default XGMI) with ``fit_ok`` and the medians
+    attached.  Only a trustworthy fit (>= FIT_MIN_SIZES sizes, slope > 0,
+    intercept >= 0, R^2 >= FIT_MIN_R2) replaces the stated latency and
+    bandwidth; otherwise ``fit_ok`` is False, the stated values stay and
+    ``prune`` keeps every candidate (round 5's 8-rank rehearsal fitted a
+    negative slope from two noisy points and set the latency to 20.6 ms,
+    which pruned four candidates untimed)."""
     out = dict(base or XGMI)
-    pts = [(float(b), float(t)) for b, t in points if t > 0]
-    if not pts:
+    by_size: Dict[float, List[float]] = {}
+    for b, t in points:
+        if t > 0:
+            by_size.setdefault(float(b), []).append(float(t))
+    med = sorted((b, sorted(ts)[len(ts) // 2] if len(ts) % 2 else
+                  0.5 * (sorted(ts)[len(ts) // 2 - 1] + sorted(ts)[len(ts) // 2]))
+                 for b, ts in by_size.items())
+    out["measured"] = [[int(b), round(t * 1e6, 3)] for b, t in med]
+    out["fit_ok"] = False
+    if len(med) < 2:
+        out["fit_reason"] = f"{len(med)} message size(s)"
         return out
-    if len(pts) >= 2 and max(b for b, _ in pts) > min(b for b, _ in pts):
-        n = len(pts)
-        mb = sum(b for b, _ in pts) / n
-        mt = sum(t for _, t in pts) / n
-        sxx = sum((b - mb) ** 2 for b, _ in pts)
-        slope = sum((b - mb) * (t - mt) for b, t in pts) / sxx
-        lat = mt - slope * mb
-        if slope > 0:
-            out["link_gbps"] = round(1.0 / slope / 1e9, 3)
-        out["latency_us"] = round(max(lat, 0.0) * 1e6, 3)
+    n = len(med)
+    mb = sum(b for b, _ in med) / n
+    mt = sum(t for _, t in med) / n
+    sxx = sum((b - mb) ** 2 for b, _ in med)
+    syy = sum((t - mt) ** 2 for _, t in med)
+    sxy = sum((b - mb) * (t - mt) for b, t in med)
+    slope = sxy / sxx
+    lat = mt - slope * mb
+    r2 = (sxy * sxy / (sxx * syy)) if syy > 0 else 1.0
+    out["fit_r2"] = round(r2, 4)
+    if n < FIT_MIN_SIZES:
+        out["fit_reason"] = f"{n} message sizes (< {FIT_MIN_SIZES})"
+    elif slope <= 0:
+        out["fit_reason"] = "non-positive slope"
+    elif lat < 0:
+        out["fit_reason"] = "negative latency"
+    elif r2 < FIT_MIN_R2:
+        out["fit_reason"] = f"R^2 {r2:.3f} < {FIT_MIN_R2}"
     else:
-        b, t = pts[0]
-        out["latency_us"] = round(max(t - b / (out["link_gbps"] * 1e9), 0.0) * 1e6, 3)
-    out["measured"] = [[int(b), round(t * 1e6, 3)] for b, t in pts]
+        out["fit_ok"] = True
+        out["link_gbps"] = round(1.0 / slope / 1e9, 3)
+        out["latency_us"] = round(lat * 1e6, 3)
     return out
 
 
@@ -154,6 +223,10 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
     lx = math.ceil(cfg.nx / px)
     ly = math.ceil(cfg.ny / py)
     m = cfg.halo_passes or halo_passes
+    if not cfg.halo_passes and world > 1:
+        rm = resident_halo_passes(cfg.nx, cfg.ny, px, py, depth)
+        if rm >= RES_MIN_PASSES:
+            m = rm
     if world == 1:
         m = 1
     schedule = cfg.schedule if cfg.schedule != "auto" else "sync"
@@ -204,13 +277,22 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
 
 def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3,
           xgmi: Dict = None) -> List[HeatConfig]:
-    """The candidates whose predicted time is within `slack` x the best
-    prediction (the autotune times only these); `xgmi` as in predict."""
-    if len(cands) <= 1:
+    """The candidates the autotune times: those whose predicted time is
+    within `slack` x the best prediction, plus the best-predicted candidate
+    of every (layout, passes per exchange) pair, so a model error can cost a
+    schedule but never a whole layout or halo depth.  With a measured
+    exchange fit that failed its quality checks (``xgmi["fit_ok"]`` False)
+    nothing is pruned."""
+    if len(cands) <= 1 or (xgmi is not None and not xgmi.get("fit_ok", True)):
         return list(cands)
     t = [predict(c, world, xgmi=xgmi)["ms_per_1000"] for c in cands]
     best = min(t)
-    return [c for c, x in zip(cands, t) if x <= slack * best]
+    group_best: Dict[tuple, float] = {}
+    for c, x in zip(cands, t):
+        k = (_grid(c, world), c.halo_passes)
+        group_best[k] = min(group_best.get(k, float("inf")), x)
+    return [c for c, x in zip(cands, t)
+            if x <= slack * best or x == group_best[(_grid(c, world), c.halo_passes)]]
 
 
 def model_params(xgmi: Dict = None) -> Dict:

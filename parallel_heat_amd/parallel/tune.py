@@ -66,26 +66,36 @@ def describe(cfg: HeatConfig, world: int) -> Dict[str, object]:
     return {"px": px, "py": py, "schedule": cfg.schedule, "halo_passes": cfg.halo_passes}
 
 
-def measure_exchange(solver, depths: Sequence[int], iters: int = 20,
+def exchange_depths(halo: int) -> List[int]:
+    """Three (or more) distinct probe depths up to `halo`: H, H/2, H/4."""
+    return sorted({max(1, halo), max(1, halo // 2), max(1, halo // 4)})
+
+
+def measure_exchange(solver, depths: Sequence[int], iters: int = 20, reps: int = 5,
                      agree_max: Optional[Callable[[float], float]] = None) -> List[tuple]:
-    """(largest message bytes, seconds per grouped exchange) of `solver`'s halo
-    exchange at each depth (<= its halo), timed on the real ranks; `agree_max`
-    reduces a float to its max over the ranks (the slowest rank sets the
-    pace).  Collective.  Feed the points to parallel.model.fit_exchange."""
+    """(largest message bytes, seconds per grouped exchange) samples of
+    `solver`'s halo exchange at each depth (<= its halo): `reps` samples of
+    `iters` exchanges each, interleaved over the depths (a slow phase of the
+    machine hits every size), timed on the real ranks; `agree_max` reduces a
+    float to its max over the ranks (the slowest rank sets the pace).
+    Collective.  Feed the samples to parallel.model.fit_exchange, which takes
+    the median per size."""
     out = []
-    for d in depths:
-        d = max(1, min(int(d), solver.info.halo))
-        t, b = solver.time_exchange(d, iters)
-        if agree_max is not None:
-            t = agree_max(t)
-        out.append((b, t))
+    ds = [max(1, min(int(d), solver.info.halo)) for d in depths]
+    for _ in range(reps):
+        for d in ds:
+            t, b = solver.time_exchange(d, iters)
+            if agree_max is not None:
+                t = agree_max(t)
+            out.append((b, t))
     return out
 
 
 def is_clean_failure(e: BaseException) -> bool:
     """A run-time failure after which the rank's queued work completed and its
-    communicator was kept (the native run() says "[clean]"): every rank meets
-    it at the same point, so the ranks can agree and go on."""
+    communicator was kept (the native run() says "[clean]", only for
+    heat::GlobalError, e.g. a non-finite all-reduced residual): every rank
+    meets it at the same point, so the ranks can agree and go on."""
     return "[clean]" in str(e)
 
 
@@ -107,8 +117,8 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
 
     * rejects it at construction,
     * fails at run time "cleanly" (the native run() drained its queued work
-      and kept the communicator: a planning check or a non-finite residual,
-      which every rank meets at the same point), or
+      and kept the communicator: an error class every rank meets at the same
+      point, heat::GlobalError -- a non-finite all-reduced residual), or
     * reports a resident-tile give-up (HEAT_TB_RES_GIVEUP=defer: the run's
       results are invalid, its transport calls all matched).
 
@@ -198,56 +208,60 @@ def autotune(cfg: HeatConfig, info: DistInfo, candidates: Optional[List[HeatConf
             return False
         return True
 
-    for c in candidates:
-        row = describe(c, world)
-        solver = None
-        try:
-            solver = make(c)
-            ok = 1.0
-        except _native.NativeError as e:
-            ok = 0.0
-            row["error"] = str(e).splitlines()[0][:200]
-        if agree_all(ok, MIN) < 1.0:
-            if solver is not None:
-                solver.close()
-            row.setdefault("error", "rejected on another rank")
+    # The gloo group is destroyed on every exit (a raise included: bench.py
+    # may call autotune again after a failure).
+    try:
+        for c in candidates:
+            row = describe(c, world)
+            solver = None
+            try:
+                solver = make(c)
+                ok = 1.0
+            except _native.NativeError as e:
+                ok = 0.0
+                row["error"] = str(e).splitlines()[0][:200]
+            if agree_all(ok, MIN) < 1.0:
+                if solver is not None:
+                    solver.close()
+                row.setdefault("error", "rejected on another rank")
+                table.append(row)
+                if log:
+                    log(f"autotune: {row} skipped")
+                continue
+            # Untimed run (graph capture, RCCL connections); the agreement after
+            # it is also the barrier before the timed runs.
+            ok = attempt(solver, row, lambda: solver.run(steps).resident_giveups > 0)
+            if not agree_ok(solver, row, ok):
+                continue
+            sync()
+            t0 = time.perf_counter()
+
+            def timed():
+                g = 0
+                for _ in range(repeats):
+                    g += solver.run(steps).resident_giveups
+                return g > 0
+
+            ok = attempt(solver, row, timed)
+            sync()
+            dt = time.perf_counter() - t0
+            if not agree_ok(solver, row, ok):
+                continue
+            row["halo"] = solver.info.halo
+            row["tb_depth"] = solver.info.tb_depth
+            solver.close()
+            dt = agree_all(dt, MAX)
+            ms = dt * 1e3 * 1000.0 / (steps * repeats)
+            row["ms_per_1000_iters"] = round(ms, 4)
+            row["repeats"] = repeats
             table.append(row)
             if log:
-                log(f"autotune: {row} skipped")
-            continue
-        # Untimed run (graph capture, RCCL connections); the agreement after
-        # it is also the barrier before the timed runs.
-        ok = attempt(solver, row, lambda: solver.run(steps).resident_giveups > 0)
-        if not agree_ok(solver, row, ok):
-            continue
-        sync()
-        t0 = time.perf_counter()
-
-        def timed():
-            g = 0
-            for _ in range(repeats):
-                g += solver.run(steps).resident_giveups
-            return g > 0
-
-        ok = attempt(solver, row, timed)
-        sync()
-        dt = time.perf_counter() - t0
-        if not agree_ok(solver, row, ok):
-            continue
-        row["halo"] = solver.info.halo
-        row["tb_depth"] = solver.info.tb_depth
-        solver.close()
-        dt = agree_all(dt, MAX)
-        ms = dt * 1e3 * 1000.0 / (steps * repeats)
-        row["ms_per_1000_iters"] = round(ms, 4)
-        row["repeats"] = repeats
-        table.append(row)
-        if log:
-            log(f"autotune: {row}")
-        if ms < best_ms:
-            best, best_ms = c, ms
-    if group is not None:
-        dist.destroy_process_group(group)
+                log(f"autotune: {row}")
+            if ms < best_ms:
+                best, best_ms = c, ms
+    finally:
+        if group is not None:
+            dist.destroy_process_group(group)
     if best is None:
         raise _native.NativeError("autotune: every candidate was rejected: %r" % table)
     return best, table

@@ -192,6 +192,28 @@ def test_cli_memory_plan(tmp_path):
     assert not huge["fits_288gb"]
 
 
+def test_cli_plan_resident_aware_halo(tmp_path):
+    # Passes per exchange follow resident fit (plan.hpp resident_halo_passes,
+    # the same rule as the solver and parallel/model.py): 8192^2 on 2 x 2
+    # ranks takes m = 5 (4144-cell span boxes, 20 x 16 resident tiles) instead
+    # of m = 8 (4180: no one-round plan); slabs whose only fitting m is below
+    # kResMinPasses keep m = 8; --halo-passes overrides.
+    from parallel_heat_amd.parallel.model import resident_halo_passes
+    want = {("auto", 4): (5, True), ("rows", 4): (8, False), ("auto", 8): (8, True),
+            ("rows", 8): (8, True), ("auto", 2): (8, False)}
+    for (decomp, g), (m, res) in want.items():
+        p = json.loads(heat(["--nx", "8192", "--ny", "8192", "--gpus", str(g), "--decomp", decomp,
+                             "--plan"], tmp_path).stdout)
+        assert (p["halo_passes"], p["resident"]) == (m, res), (decomp, g, p)
+        assert p["halo"] == 12 * m
+        px, py = map(int, p["process_grid"].split("x"))
+        rm = resident_halo_passes(8192, 8192, px, py)
+        assert m == (rm if rm >= 4 else 8)
+    forced = json.loads(heat(["--nx", "8192", "--ny", "8192", "--gpus", "4", "--halo-passes", "8",
+                              "--plan"], tmp_path).stdout)
+    assert forced["halo_passes"] == 8 and not forced["resident"]
+
+
 def _flags_of(text):
     import re
     return set(re.findall(r"(?<![\w-])(--[a-z][a-z0-9-]*)", text))

@@ -141,3 +141,18 @@ def test_rccl_dead_peer_fails_fast(gpu, tmp_path):
     assert procs[0].returncode != 0, (out0[-500:], err0[-2000:])
     assert "no progress" in err0 or "RCCL" in err0 or "aborted" in err0, err0[-2000:]
     assert elapsed < 60
+
+
+def test_rccl_abort_while_calls_run(gpu):
+    # RcclTransport::abort() freed the communicator while
+    # another thread could be between its liveness check and its next RCCL
+    # call.  Calls now announce themselves and re-check the abort flag; an
+    # abort waits for calls already inside RCCL.  20 rounds of a thread
+    # issuing send/recv + all-reduce back to back while this thread aborts:
+    # every round ends with the worker's calls refused, nothing crashes.
+    import ctypes
+
+    from parallel_heat_amd import _native
+    calls = ctypes.c_int()
+    _native.call("heat_rccl_abort_race_test", 0, 20, ctypes.byref(calls))
+    assert calls.value > 0

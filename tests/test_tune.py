@@ -184,22 +184,83 @@ def test_autotune_two_ranks_agree_on_skips(tmp_path):
 
 
 def test_fit_exchange_and_prune_from_measurements():
-    # Latency and link bandwidth fitted from measured (bytes, seconds) points
-    # replace the stated constants in predict() and prune().
+    # Latency and link bandwidth fitted from measured (bytes, seconds) samples
+    # (median per size) replace the stated constants in predict() and prune().
     from parallel_heat_amd.parallel.model import XGMI, fit_exchange, predict, prune
-    pts = [(3_000_000, 12e-6 + 3_000_000 / 20e9), (750_000, 12e-6 + 750_000 / 20e9)]
+    sizes = (3_000_000, 1_500_000, 750_000)
+    pts = [(b, 12e-6 + b / 20e9) for b in sizes for _ in range(4)]
+    pts.append((750_000, 5e-3))  # one outlier sample: the median ignores it
     x = fit_exchange(pts)
+    assert x["fit_ok"] and x["fit_r2"] > 0.999
     assert abs(x["link_gbps"] - 20.0) < 0.01 and abs(x["latency_us"] - 12.0) < 0.01
-    assert x["measured"][0] == [3_000_000, round(pts[0][1] * 1e6, 3)]
+    assert x["measured"][-1] == [3_000_000, round(pts[0][1] * 1e6, 3)]
     assert XGMI["link_gbps"] == 50.0  # the stated model is untouched
-    one = fit_exchange([(1_000_000, 40e-6)])  # one point: stated GB/s, latency = rest
-    assert abs(one["latency_us"] - 20.0) < 1e-6
     cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
     cands = default_candidates(cfg, 8, schedules=["sync", "pipeline"], halo_passes=[0, 4])
     p_stated, p_meas = predict(cands[0], 8), predict(cands[0], 8, xgmi=x)
     assert p_meas["exchange_ms"] > p_stated["exchange_ms"]
     # Very slow links (1 GB/s) make the 1-D slabs' 3 MB messages the cost:
-    # the 2-D grid's smaller messages win and the slabs are pruned.
-    slow = fit_exchange([(3_000_000, 3_000_000 / 1e9), (750_000, 750_000 / 1e9)])
+    # the 2-D grid's smaller messages win; the slabs' candidates fall outside
+    # the slack, but the best one of each (layout, halo passes) is still timed.
+    slow = fit_exchange([(b, b / 1e9 + 1e-6) for b in sizes])
+    assert slow["fit_ok"]
     kept = [tuple(describe(c, 8).values()) for c in prune(cands, 8, xgmi=slow)]
-    assert kept and all(k[:2] == (4, 2) for k in kept), kept
+    assert {(k[0], k[1], k[3]) for k in kept} == {(8, 1, 0), (8, 1, 4), (4, 2, 0), (4, 2, 4)}
+    assert len(kept) < len(cands)
+
+
+def test_fit_exchange_rejects_round5_rehearsal_points():
+    # The round-5 8-rank rehearsal (8 RCCL ranks on one GPU over sockets)
+    # measured 19,942 us at 0.83 MB and 17,799 us at 3.3 MB: a negative
+    # slope.  Its fit then kept 50 GB/s, set the latency to 20.6 ms and
+    # pruned four candidates untimed.  Now: not trusted, nothing pruned.
+    from parallel_heat_amd.parallel.model import XGMI, fit_exchange, prune
+    pts = [(829440, 19942.334e-6), (3317760, 17799.033e-6)]
+    x = fit_exchange(pts)
+    assert not x["fit_ok"] and "sizes" in x["fit_reason"]
+    assert x["latency_us"] == XGMI["latency_us"] and x["link_gbps"] == XGMI["link_gbps"]
+    three = fit_exchange(pts + [(1658880, 21000e-6)])
+    assert not three["fit_ok"] and three["fit_reason"] == "non-positive slope"
+    noisy = fit_exchange([(1e6, 50e-6), (2e6, 20e-6), (3e6, 90e-6), (4e6, 60e-6)])
+    assert not noisy["fit_ok"] and noisy["fit_reason"].startswith("R^2")
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    cands = default_candidates(cfg, 8, schedules=["sync", "pipeline"], halo_passes=[0, 4])
+    for bad in (x, three, noisy):
+        assert prune(cands, 8, xgmi=bad) == cands
+
+
+def test_measure_exchange_interleaves_three_sizes():
+    from parallel_heat_amd.parallel.tune import exchange_depths, measure_exchange
+    assert exchange_depths(96) == [24, 48, 96] and exchange_depths(2) == [1, 2]
+    calls = []
+
+    class S:
+        info = type("I", (), {"halo": 96})()
+
+        def time_exchange(self, d, iters):
+            calls.append((d, iters))
+            return 1e-5 * d, d * 1000
+
+    pts = measure_exchange(S(), exchange_depths(96), iters=20, reps=5)
+    assert len(pts) == 15 and calls[:3] == [(24, 20), (48, 20), (96, 20)]
+    assert {b for b, _ in pts} == {24000, 48000, 96000}
+
+
+def test_resident_aware_halo_passes_model():
+    # The solver's resident-aware m (topology.cpp resident_halo_passes,
+    # mirrored by the model): 2 x 2 at 8192^2 -> m = 5 (4144-cell span boxes
+    # in 20 x 16 tiles; m = 8 gives 4180, which has no one-round plan); the
+    # 1-D 4-rank slabs fit only at m = 2 (< RES_MIN_PASSES: m = 8 streaming);
+    # 8 ranks keep m = 8.
+    from parallel_heat_amd.parallel.model import RES_MIN_PASSES, predict, resident_halo_passes
+    assert resident_halo_passes(8192, 8192, 2, 2) == 5
+    assert resident_halo_passes(8192, 8192, 4, 1) == 2 < RES_MIN_PASSES
+    assert resident_halo_passes(8192, 8192, 8, 1) == 8
+    assert resident_halo_passes(8192, 8192, 4, 2) == 8
+    assert resident_halo_passes(8192, 8192, 2, 1) == 0  # 4096 x 8192 has no resident plan
+    cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
+    p = predict(cfg.replace(decomp="auto"), 4)
+    assert p["layout"] == "2x2" and p["halo"] == 60 and p["resident"]
+    assert p["tcells_per_s"] > 16.0
+    rows = predict(cfg.replace(decomp="rows"), 4)
+    assert rows["halo"] == 96 and not rows["resident"]
