@@ -17,12 +17,20 @@ HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LDFLAGS := -fopenmp -L$(ROCM)/lib -lrccl -ldl -Wl,-rpath,$(ROCM)/lib
 
 SRCS_CPP := $(wildcard csrc/src/*.cpp)
-SRCS_HIP := $(wildcard csrc/kernels/*.hip)
+# Experiment kernels (csrc/kernels/tb_exp.hpp): builds measured slower than
+# the defaults, kept for A/Bs and their bitwise tests in their own library
+# (`make exp` -> libheat_exp.so, loaded on demand), not in libheat.so.
+EXP_HIP  := csrc/kernels/tb_packed.hip csrc/kernels/tb_narrow.hip csrc/kernels/tb_split_mixed.hip \
+            csrc/kernels/tb_split_pk.hip csrc/kernels/tb_chain.hip csrc/kernels/exp_register.hip
+SRCS_HIP := $(filter-out $(EXP_HIP),$(wildcard csrc/kernels/*.hip))
+EXP_OBJS := $(patsubst csrc/kernels/%.hip,$(BUILD)/obj/%.o,$(EXP_HIP))
 HDRS     := $(wildcard csrc/include/heat/*.hpp csrc/include/heat/*.h)
 OBJS     := $(patsubst csrc/src/%.cpp,$(BUILD)/obj/%.o,$(SRCS_CPP)) \
             $(patsubst csrc/kernels/%.hip,$(BUILD)/obj/%.o,$(SRCS_HIP))
 
 all: $(LIBDIR)/libheat.so $(BUILD)/heat
+
+exp: $(LIBDIR)/libheat_exp.so
 
 # Header dependencies come from the compiler (-MMD): a header edit rebuilds
 # only the objects that include it (the TB kernel builds take minutes each).
@@ -36,23 +44,30 @@ $(BUILD)/obj/tb_scalar.o $(BUILD)/obj/tb_split.o $(BUILD)/obj/tb_tile.o $(BUILD)
   $(BUILD)/obj/tb_tile_xl0.o $(BUILD)/obj/tb_tile_xl1.o $(BUILD)/obj/tb_tile_xl2.o \
   $(BUILD)/obj/tb_resident_xl0.o $(BUILD)/obj/tb_resident_xl1.o $(BUILD)/obj/tb_resident_xl2.o \
   $(BUILD)/obj/tb_split_rla.o $(BUILD)/obj/tb_split_rlb.o $(BUILD)/obj/tb_split_rlc.o \
-  $(BUILD)/obj/tb_split_mixed.o $(BUILD)/obj/tb_split_nt.o $(BUILD)/obj/tb_chain.o: HIPFLAGS += -fno-slp-vectorize
+  $(BUILD)/obj/tb_split_mixed.o $(BUILD)/obj/tb_split_nt.o $(BUILD)/obj/tb_split_pk.o \
+  $(BUILD)/obj/tb_chain.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/obj/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(DEPFLAGS) -c $< -o $@
 
--include $(OBJS:.o=.d)
+-include $(OBJS:.o=.d) $(EXP_OBJS:.o=.d)
 # An object without its .d file (built before -MMD, or never built) depends
 # on every header: a shared-header edit can never link objects built against
 # two layouts of one struct (TbArgs).
-$(foreach o,$(OBJS),$(if $(wildcard $(o:.o=.d)),,$(eval $(o): $(HDRS) $(KHDRS))))
+$(foreach o,$(OBJS) $(EXP_OBJS),$(if $(wildcard $(o:.o=.d)),,$(eval $(o): $(HDRS) $(KHDRS))))
 
 # Linked under a temporary name and renamed: a copy of the tree taken while
 # a build runs holds the old library or the new one, never a partial file.
 $(LIBDIR)/libheat.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@.tmp $(OBJS) $(LDFLAGS) && mv -f $@.tmp $@
+
+# The experiment kernels link against the product library (the registry and
+# every shared helper live there; rpath $ORIGIN: the copy next to it).
+$(LIBDIR)/libheat_exp.so: $(EXP_OBJS) $(LIBDIR)/libheat.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@.tmp $(EXP_OBJS) -L$(LIBDIR) -l:libheat.so \
+	  -Wl,-rpath,'$$ORIGIN' $(LDFLAGS) && mv -f $@.tmp $@
 
 $(BUILD)/heat: csrc/apps/heat_main.cpp $(OBJS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip csrc/apps/heat_main.cpp -x none $(OBJS) -o $@.tmp $(LDFLAGS) && mv -f $@.tmp $@
@@ -77,9 +92,9 @@ resources: $(LIBDIR)/libheat.so
 	python3 tools/kernel_resources.py $(LIBDIR)/libheat.so
 
 clean:
-	rm -rf $(BUILD) $(LIBDIR)/libheat.so
+	rm -rf $(BUILD) $(LIBDIR)/libheat.so $(LIBDIR)/libheat_exp.so
 
-.PHONY: all asm resources clean
+.PHONY: all exp asm resources clean
 
 # Host-only self-test of the CPU components, plain and under ASan/UBSan.
 SELFTEST_SRCS := csrc/tests/selftest.cpp csrc/src/common.cpp csrc/src/topology.cpp \

@@ -34,6 +34,7 @@
 #include "heat/init_fn.hpp"
 #include "heat/kernels.hpp"
 #include "tb_common.hpp"
+#include "tb_exp.hpp"
 #include "tb_tile.hpp"
 
 namespace heat::gpu {
@@ -395,15 +396,16 @@ int tb_resident_waves(int depth, int variant) {
   const int lag = tb_variant_lag(variant);
   if (tb_variant_split(variant)) {
     // Work units are two-wave pipelines, two per block.
-    const int occ = (variant & tbv::kShiftMixed) ? tbxm::occupancy_split(depth)
-                                                 : tbx::occupancy_split(depth);
+    const int occ = (variant & tbv::kShiftMixed)
+                        ? tb_exp("the mixed-shift split build (kShiftMixed)").tbxm_occupancy_split(depth)
+                        : tbx::occupancy_split(depth);
     const int w = std::max(1, cus * std::max(1, occ) * 2);
     cache.emplace(key, w);
     return w;
   }
-  const int per_cu = (variant & tbv::kFloat2)  ? tbn::occupancy(depth, lag)
+  const int per_cu = (variant & tbv::kFloat2)  ? tb_exp("the float2-lane build (kFloat2)").tbn_occupancy(depth, lag)
                      : (variant & tbv::kScalar) ? tbs::occupancy(depth, lag)
-                                                : tbp::occupancy(depth, lag);
+                                                : tb_exp("the packed build (no kScalar)").tbp_occupancy(depth, lag);
   const int w = std::max(1, cus * std::max(1, per_cu) * 4);
   cache.emplace(key, w);
   return w;
@@ -492,6 +494,34 @@ bool tb_mid_residual(int depth) {
   // pipelines (tb_split_rl*.hip) or the workgroup tiles (tb_tile.hip), which
   // take a residual at any inner step; forced variants keep the last step.
   return depth == kTbDeepDepth && tb_tuning().variant < 0;
+}
+
+namespace {
+std::mutex g_exp_mu;
+const TbExpKernels* g_exp = nullptr;
+}  // namespace
+
+bool tb_exp_loaded() {
+  std::lock_guard<std::mutex> lk(g_exp_mu);
+  return g_exp != nullptr;
+}
+
+const TbExpKernels& tb_exp(const char* what) {
+  std::lock_guard<std::mutex> lk(g_exp_mu);
+  HEAT_CHECK(g_exp != nullptr,
+             "%s is an experiment kernel build: `make exp`, then load "
+             "parallel_heat_amd/_lib/libheat_exp.so (HEAT_EXP=1)", what);
+  return *g_exp;
+}
+
+// HEAT_TB_SPLIT_PK=1: the streaming level-split launches take the packed-f32
+// build (round-6 A/B, an experiment build).
+bool split_pk_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT_TB_SPLIT_PK");
+    return e && *e && *e != '0';
+  }();
+  return on;
 }
 
 // Field bytes one pass must sweep before the level-split launches stream
@@ -795,7 +825,7 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
     const int G = (args.flags & tbdetail::kTbAgePairs) ? args.age_groups : 1;
     int blocks = (args.total_waves + 1) / 2;
     if (G > 1) blocks = (blocks + 7) / 8 * 8 * G;
-    static const int occ = tbc::occupancy_chain(kTbDeepDepth);  // one device model (gfx950)
+    static const int occ = tb_exp("the chained build (HEAT_TB_CHAIN=1)").tbc_occupancy_chain(kTbDeepDepth);
     int dev = 0, cus = 0;
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -816,18 +846,30 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
       tb_trace_once(line);
     }
     if (fits) {
-      chain->chained = tbc::launch_chain(args, depth, chain->passes, chain->flags, chain->done,
-                                         chain->err, st);
+      chain->chained = tb_exp("the chained build (HEAT_TB_CHAIN=1)")
+                           .tbc_launch_chain(args, depth, chain->passes, chain->flags, chain->done,
+                                             chain->err, st);
       HIP_CHECK(hipGetLastError());
       return;
     }
   }
-  const bool ok = split ? ((variant & tbv::kShiftMixed)                ? tbxm::launch_split(args, depth, st)
-                           : (args.flags & tbdetail::kTbStreamRows) ? tbxn::launch_split(args, depth, st)
-                                                                      : tbx::launch_split(args, depth, st))
-                  : (variant & tbv::kFloat2) ? tbn::launch(args, depth, lag, st)
-                  : (variant & tbv::kScalar) ? tbs::launch(args, depth, lag, st)
-                                             : tbp::launch(args, depth, lag, st);
+  bool ok;
+  if (split) {
+    if (variant & tbv::kShiftMixed)
+      ok = tb_exp("the mixed-shift split build (kShiftMixed)").tbxm_launch_split(args, depth, st);
+    else if (!(args.flags & tbdetail::kTbStreamRows))
+      ok = tbx::launch_split(args, depth, st);
+    else if (split_pk_enabled())
+      ok = tb_exp("the packed split build (HEAT_TB_SPLIT_PK=1)").tbxnp_launch_split(args, depth, st);
+    else
+      ok = tbxn::launch_split(args, depth, st);
+  } else if (variant & tbv::kFloat2) {
+    ok = tb_exp("the float2-lane build (kFloat2)").tbn_launch(args, depth, lag, st);
+  } else if (variant & tbv::kScalar) {
+    ok = tbs::launch(args, depth, lag, st);
+  } else {
+    ok = tb_exp("the packed build (no kScalar)").tbp_launch(args, depth, lag, st);
+  }
   HEAT_CHECK(ok, "TB depth %d is not instantiated for variant %d (depth %d: scalar ring-3+ramp only)",
              depth, variant, kTbDeepDepth);
   HIP_CHECK(hipGetLastError());
@@ -902,7 +944,7 @@ void residual_box(const float* a, const float* b, int64_t pitch, const Box& box,
 
 }  // namespace heat::gpu
 
-// The packed-update build of the temporally blocked kernel.
-#define HEAT_TB_NS tbp
-#define HEAT_TB_PACKED 1
-#include "tb_stream.inl"
+extern "C" void heat_register_exp_kernels(const heat::gpu::TbExpKernels* k) {
+  std::lock_guard<std::mutex> lk(heat::gpu::g_exp_mu);
+  heat::gpu::g_exp = k;
+}

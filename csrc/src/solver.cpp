@@ -742,7 +742,7 @@ int Solver::resident_span(const std::vector<PassPlan>& plan, size_t i) const {
         (!gated() || plan[j].rl % 2 != 0 || nchk == gpu::kTbResidentMaxChecks))
       break;
     if (n > 0 && ((ns && gr < k) || (ew && gc < k))) break;
-    if (n == res_span_max_) break;
+    if (res_span_max_ > 0 && n == res_span_max_) break;
     if (ns) gr -= k;
     if (ew) gc = round_down(gc - k, 4);
     ++n;

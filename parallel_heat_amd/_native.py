@@ -192,8 +192,9 @@ _SIGS = {
 
 
 def build_native(jobs: int = 8, quiet: bool = True) -> None:
-    """Compile libheat.so and the ``heat`` CLI for gfx950 with hipcc (``make``)."""
-    cmd = ["make", f"-j{jobs}", "-C", str(REPO_DIR)]
+    """Compile libheat.so, the ``heat`` CLI and the experiment kernels
+    (libheat_exp.so) for gfx950 with hipcc (``make all exp``)."""
+    cmd = ["make", f"-j{jobs}", "-C", str(REPO_DIR), "all", "exp"]
     res = subprocess.run(cmd, capture_output=quiet, text=True)
     if res.returncode != 0:
         raise NativeError("native build failed:\n" + (res.stdout or "") + (res.stderr or ""))
@@ -228,7 +229,30 @@ def lib():
         if L.heat_abi_version() != ABI_VERSION:
             raise NativeError("libheat ABI mismatch; rebuild with `make`")
         _lib = L
-        return _lib
+    if os.environ.get("HEAT_EXP", "") not in ("", "0"):
+        load_exp()
+    return _lib
+
+
+# The experiment kernels (csrc/kernels/tb_exp.hpp; `make exp`): TB builds
+# measured slower than the defaults, kept out of the product library and
+# registered with it when this one is loaded (HEAT_EXP=1, or load_exp()).
+EXP_PATH = LIB_PATH.parent / "libheat_exp.so"
+_exp = None
+
+
+def load_exp():
+    """Load libheat_exp.so next to the product library: its kernels (packed
+    and float2 single-wave builds, mixed-shift and packed split builds,
+    chained passes) become available to tb_step and the solver."""
+    global _exp
+    lib()
+    with _lock:
+        if _exp is None:
+            if not EXP_PATH.exists():
+                raise NativeError(f"{EXP_PATH} is missing: build it with `make exp`")
+            _exp = ctypes.CDLL(str(EXP_PATH))
+    return _exp
 
 
 def available() -> bool:
@@ -276,5 +300,5 @@ __all__ = [
     "HeatParams", "HeatComm", "HeatMsg", "HeatTransportInfo", "HeatTbTuning", "HeatRunStats", "HeatBlockInfo", "HeatChecksum",
     "SENDRECV_CB", "ALLREDUCE_CB", "BARRIER_CB", "NativeError", "lib", "call", "check",
     "available", "build_native", "loaded_path", "device_count", "rccl_unique_id",
-    "require_gpu_native", "LIB_PATH", "CLI_PATH", "c_uint",
+    "require_gpu_native", "LIB_PATH", "CLI_PATH", "c_uint", "EXP_PATH", "load_exp",
 ]

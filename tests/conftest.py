@@ -27,3 +27,12 @@ def gpu():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def exp_kernels():
+    """The experiment kernels (libheat_exp.so, `make exp`): the test files that
+    cover the measured-slower TB builds (packed, float2, mixed shifts,
+    chained passes) load them; the product library does not carry them."""
+    from parallel_heat_amd import _native
+    return _native.load_exp()

@@ -27,11 +27,12 @@ def rccl_host_per_rank(rank):
                       NCCL_IB_DISABLE="1")
 
 
-def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
+def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks, env=None):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    os.environ.update(env or {})
     if transport == "rccl":
         rccl_host_per_rank(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -47,28 +48,35 @@ def worker(rank, world, port, cfg_kwargs, steps, out_path, transport, chunks):
     if cfg_kwargs.get("init") == "zero":  # start from a grid scattered by rank 0
         from parallel_heat_amd.models import reference as R
         s.scatter(R.init_grid(cfg.nx, cfg.ny, "random", 77) if rank == 0 else None)
-    conv, conv_at, done = False, -1, 0
+    conv, conv_at, done, res_passes, giveups = False, -1, 0, 0, 0
     for n in (chunks or [steps]):
         r = s.run(n)
         done += r.steps_done
+        res_passes += r.resident_passes
+        giveups += r.resident_giveups
         if r.converged:
             conv, conv_at = True, r.converged_at
             break
     g = s.gather()
     cs = s.checksum()
+    every = [None] * world
+    dist.all_gather_object(every, [res_passes, giveups, s.info.halo])
     if rank == 0:
         np.savez(out_path, grid=g, conv=conv, conv_at=conv_at, done=done, hash=cs["hash"],
-                 px=s.info.px, py=s.info.py, exchanges=r.exchanges, schedule=s.info.schedule)
+                 px=s.info.px, py=s.info.py, exchanges=r.exchanges, schedule=s.info.schedule,
+                 resident_passes=np.array([e[0] for e in every]),
+                 resident_giveups=np.array([e[1] for e in every]),
+                 halo=np.array([e[2] for e in every]))
     s.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(world, cfg_kwargs, steps, tmp_path, transport="torch", chunks=None):
+def run_world(world, cfg_kwargs, steps, tmp_path, transport="torch", chunks=None, env=None):
     import torch.multiprocessing as mp
 
     out = str(tmp_path / f"out_{world}_{os.getpid()}.npz")
-    mp.spawn(worker, args=(world, free_port(), cfg_kwargs, steps, out, transport, chunks),
+    mp.spawn(worker, args=(world, free_port(), cfg_kwargs, steps, out, transport, chunks, env),
              nprocs=world, join=True)
     return dict(np.load(out))
 

@@ -10,7 +10,7 @@ import pytest
 
 from parallel_heat_amd import HeatConfig, HeatSolver, ops
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("exp_kernels")]
 
 
 def _run(cfg, chain, nt=-1):  # chain: HEAT_TB_CHAIN=1 (opt-in) or 0

@@ -7,7 +7,7 @@ import torch
 from parallel_heat_amd import ops
 from parallel_heat_amd.models import reference as R
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("exp_kernels")]
 
 V = ops.TbVariant
 RAMP_S = V.RAMP | V.SCALAR            # 7: scalar ring-3 + ramp

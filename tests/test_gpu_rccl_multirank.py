@@ -156,3 +156,44 @@ def test_rccl_abort_while_calls_run(gpu):
     calls = ctypes.c_int()
     _native.call("heat_rccl_abort_race_test", 0, 20, ctypes.byref(calls))
     assert calls.value > 0
+
+
+@pytest.mark.parametrize("world,kw", [
+    (2, dict(decomp="rows")),
+    (4, dict(px=2, py=2)),  # ghost corners, 2-D span boxes
+])
+def test_rccl_resident_spans_converge_inside(gpu, tmp_path, world, kw):
+    # The sequence a real multi-GPU run executes: resident-tile launches (m
+    # passes each, tiles kept in VGPRs) with grouped RCCL exchanges between
+    # them, captured in the segment graphs, checks every 20 steps inside the
+    # spans, one all-reduce + device judge per span.  Separate processes, one
+    # RCCL host id each (socket transport on one GPU); HEAT_TB_RESIDENT=2
+    # lets the ranks' small resident grids share the device (they all fit
+    # one dispatch round together).  Convergence lands at step 440 = 6 spans
+    # of 64 steps + 7 passes of 8: inside a span, replayed bit-exactly from
+    # the span's source.  Bitwise against one rank.
+    base = dict(nx=600, ny=1024, steps=20000, init="random", seed=11, backend="hip",
+                converge=True, check_interval=20, eps=1e-2, **kw)
+    res = run_world(world, base, 20000, tmp_path, transport="rccl",
+                    env={"HEAT_TB_RESIDENT": "2"})
+    ref, r, h = single(base, 20000)
+    assert r.converged and r.converged_at == 440
+    assert bool(res["conv"]) and int(res["conv_at"]) == 440 and int(res["done"]) == 440
+    assert (res["resident_passes"] > 0).all(), res["resident_passes"]
+    assert (res["resident_giveups"] == 0).all()
+    assert (res["halo"] == 64).all()  # m = 8 passes of depth 8 per exchange
+    assert np.array_equal(res["grid"], ref)
+    assert str(res["hash"]) == h
+
+
+def test_rccl_resident_spans_across_runs(gpu, tmp_path):
+    # Unchecked resident spans with exchanges, runs of odd lengths (spans cut
+    # by run ends, remainder passes), graphs replayed across runs.
+    base = dict(nx=700, ny=900, steps=0, init="random", seed=3, backend="hip", decomp="rows")
+    res = run_world(2, base, 0, tmp_path, transport="rccl", chunks=[45, 300, 129, 200],
+                    env={"HEAT_TB_RESIDENT": "2"})
+    ref, _, h = single(base, 674)
+    assert int(res["done"]) == 674
+    assert (res["resident_passes"] > 0).all() and (res["resident_giveups"] == 0).all()
+    assert np.array_equal(res["grid"], ref)
+    assert str(res["hash"]) == h

@@ -56,6 +56,22 @@ __device__ __forceinline__ f4 upd(const f4& a, const f4& b, const f4& c, float c
     e = from_right(b.x);
   }
   if (VAR & 2) { cx = 0.5f; cy = 0.5f; }
+  if constexpr ((VAR & 32) != 0) {
+    // Packed f32 (v_pk_add_f32 / v_pk_fma_f32) on the pairs (x,y), (z,w):
+    // the same per-element operations in the same order as st() (bitwise
+    // equal; Upd::apply PK in tb_tile_core.hpp, RowUpdate HEAT_TB_PACKED in
+    // tb_stream.inl): ~14 VALU per float4 row instead of 24.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 m2 = {-2.0f, -2.0f}, cx2 = {cx, cx}, cy2 = {cy, cy};
+    const f2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+    const f2 ns01 = f2{c.x, c.y} + f2{a.x, a.y}, ns23 = f2{c.z, c.w} + f2{a.z, a.w};
+    const f2 ew01 = {b.y + w, b.z + b.x}, ew23 = {b.w + b.y, e + b.z};
+    const f2 tx01 = __builtin_elementwise_fma(m2, b01, ns01), tx23 = __builtin_elementwise_fma(m2, b23, ns23);
+    const f2 ty01 = __builtin_elementwise_fma(m2, b01, ew01), ty23 = __builtin_elementwise_fma(m2, b23, ew23);
+    const f2 r01 = __builtin_elementwise_fma(cy2, ty01, __builtin_elementwise_fma(cx2, tx01, b01));
+    const f2 r23 = __builtin_elementwise_fma(cy2, ty23, __builtin_elementwise_fma(cx2, tx23, b23));
+    return f4{r01.x, r01.y, r23.x, r23.y};
+  }
   r.x = st(b.x, a.x, c.x, w, b.y, cx, cy);
   r.y = st(b.y, a.y, c.y, b.x, b.z, cx, cy);
   r.z = st(b.z, a.z, c.z, b.y, b.w, cx, cy);
@@ -163,5 +179,10 @@ int main() {
   run<6, 1, 0>(cus, clk);
   run<6, 1, 4>(cus, clk);
   run<6, 1, 1>(cus, clk);
+  // Round 6: the packed row update in that stage (ds_bpermute shifts: the
+  // split kernel's; DPP; none).
+  run<6, 1, 36>(cus, clk);
+  run<6, 1, 32>(cus, clk);
+  run<6, 1, 33>(cus, clk);
   return 0;
 }
