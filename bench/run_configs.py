@@ -102,8 +102,11 @@ def main():
                     extra = ["--gpus", "8", "--nx", "32768", "--ny", "32768", "--decomp", "2d",
                              "--schedule", "overlap"]
                     name = "c4_32768_8ranks_2d_overlap_rehearsal_1gpu"
-                d = run([cli] + extra + ["--steps", "1000", "--init", "random", "--seed", "1234",
-                                         "--out", "none", "--json"])
+                # Warm: 1000 untimed steps capture the graphs first (round 5's
+                # rows were single cold runs with the capture inside the
+                # timed steps).
+                d = run([cli] + extra + ["--steps", "1000", "--warmup", "1000", "--init", "random",
+                                         "--seed", "1234", "--out", "none", "--json"])
                 d["note"] = "N ranks as threads on ONE GPU (loopback transport); not an N-GPU number"
             elif c == 4 and ng >= 8:
                 d = run(bench(8, ["--nx", "32768", "--ny", "32768", "--decomp", "2d",

@@ -66,6 +66,8 @@ void usage() {
       "  --phase-timing          per-phase times (exchange/compute/reduce) in --json; eager\n"
       "  --plan                  print the per-GPU memory plan (fields + halo buffers, worst\n"
       "                          rank, 288 GB HBM3E check) for --gpus/WORLD_SIZE ranks; exit\n"
+      "  --warmup N              N untimed steps first (graph capture), then the initial\n"
+      "                          state is restored and the timed run starts     [0]\n"
       "  --json                  print a JSON metrics line\n");
 }
 
@@ -80,6 +82,7 @@ struct Options {
   std::string out, out_format = "dat", naming = "plain";
   std::string checkpoint, resume;
   int64_t ckpt_every = 0;
+  int64_t warmup = 0;  // untimed steps first (graph capture, first touch), then the state is reset
   bool json = false, dump_initial = false;
 };
 
@@ -172,6 +175,14 @@ void run_rank(const Options& o, const Params& P, std::unique_ptr<Transport> tr,
       if (root) write_dat(path, P.nx, P.ny, g.data());
     }
   };
+  if (o.warmup > 0) {
+    // Untimed warm-up: the segment graphs are captured and the fields
+    // touched, then the initial state is restored (the graph cache stays),
+    // so the timed run and the output are those of a cold run.
+    HEAT_CHECK(o.resume.empty(), "--warmup with --resume");
+    (void)S.run(o.warmup);
+    S.reset();
+  }
   if (o.dump_initial || o.naming == "mpi") emit(init_path);
 
   const int64_t total = S.configured_steps(o.steps);
@@ -329,6 +340,7 @@ int main(int argc, char** argv) {
     else if (a == "--watchdog") setenv("HEAT_WATCHDOG_S", need().c_str(), 1);
     else if (a == "--port") port = std::atoi(need().c_str());
     else if (a == "--json") o.json = true;
+    else if (a == "--warmup") o.warmup = std::atoll(need().c_str());
     else if (a == "--gpus") gpus = std::atoi(need().c_str());
     else if (a == "--phase-timing") P.phase_timing = true;
     else if (a == "--plan") plan = true;

@@ -72,6 +72,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--checkpoint", default=None)
     a("--checkpoint-every", type=int, default=0)
     a("--resume", default=None)
+    a("--warmup", type=int, default=0,
+      help="N untimed steps first (graph capture), then the initial state is restored")
     a("--json", action="store_true")
     return p
 
@@ -136,6 +138,13 @@ def main(argv=None) -> int:
             if root:
                 hio.write_dat(path, g)
 
+    if args.warmup > 0:
+        # Untimed warm-up (graph capture, first touch), then the initial
+        # state again: the timed run and the output are a cold run's.
+        if args.resume:
+            raise SystemExit("--warmup with --resume")
+        solver.run(args.warmup)
+        solver.reset()
     if args.dump_initial or args.naming == "mpi":
         emit(init_path)
     total = cfg.total_steps()

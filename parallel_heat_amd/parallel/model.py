@@ -68,6 +68,14 @@ STREAM_POINTS: List[tuple] = [
 ]
 RATE_POINTS = STREAM_POINTS  # the large-block end (1 GPU) is a stream plate
 
+# A resident span of m passes pays one whole-tile load and store (what a
+# per-pass tile launch pays every pass): a rank's resident rate at m passes
+# per exchange is the long-span plate rate above / (1 + SPAN_COST / m).
+# Round-6 plates with the span capped (HEAT_TB_RES_SPAN, profiles/r6_raw/r6d):
+# 4144^2 (20 x 16 tiles) 5.37 long, 4.84 / 4.78 / 4.54 / 4.22 at 5 / 4 / 3 /
+# 2 passes (fit: 0.55); 1192 x 8192 (14 x 8) 4.29 long, 3.90 at 8 (0.8).
+SPAN_COST = 0.7
+
 SIMDS = 1024
 STRIP_COLS = 232  # useful columns per 256-column strip at depth 12
 CUS = 256
@@ -240,6 +248,8 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
     ext_c = (2 if py > 2 else 1) * (H - depth) if py > 1 else 0
     resident = schedule == "sync" and resident_fits(lx + ext_r, ly + ext_c, depth)
     rate = rate_tcells(lx, ly, resident) * 1e12
+    if resident and world > 1:
+        rate /= 1.0 + SPAN_COST / m
     cells = (lx + ext_r) * (ly + ext_c)
     compute_s = cells * 1000 / rate
     exchanges = math.ceil(1000 / H) if world > 1 else 0
@@ -297,5 +307,6 @@ def prune(cands: Sequence[HeatConfig], world: int, slack: float = 1.3,
 
 def model_params(xgmi: Dict = None) -> Dict:
     return {"xgmi": dict(xgmi or XGMI), "resident_points": [list(p) for p in RESIDENT_POINTS],
+            "span_cost": SPAN_COST,
             "stream_points": [list(p) for p in STREAM_POINTS],
             "strip_cols": STRIP_COLS, "simds": SIMDS}

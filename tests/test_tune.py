@@ -261,6 +261,6 @@ def test_resident_aware_halo_passes_model():
     cfg = HeatConfig(nx=8192, ny=8192, steps=0, backend="cpu")
     p = predict(cfg.replace(decomp="auto"), 4)
     assert p["layout"] == "2x2" and p["halo"] == 60 and p["resident"]
-    assert p["tcells_per_s"] > 16.0
+    assert p["tcells_per_s"] > 15.0  # m = 5 spans: 5.29 / (1 + 0.7 / 5) per rank
     rows = predict(cfg.replace(decomp="rows"), 4)
     assert rows["halo"] == 96 and not rows["resident"]

@@ -5,7 +5,7 @@
 
 Input: one rocprofv3 output per rank (`--kernel-trace --marker-trace
 --output-format csv -o rank_%pid%`, each rank of the torchrun job under its own
-rocprofv3; tools/sessions_r5g.sh).  Ranks are told apart by their process ids
+rocprofv3; tools/sessions/sessions_r5g.sh).  Ranks are told apart by their process ids
 and numbered in pid order.  Each kernel is classed as
 
   exchange  RCCL kernels (ncclDevKernel*, the grouped send/recv and the
