@@ -144,12 +144,22 @@ __device__ __forceinline__ float to_vgpr(float x) {
   return r;
 }
 
-// One input row element of this lane.
-__device__ __forceinline__ vecf ld_in(const float* p) {
-#if HEAT_TB_NTLOAD
-  return __builtin_nontemporal_load(reinterpret_cast<const vecf*>(p));
+// One input row element of this lane: row `rowp` (the strip's first
+// column), lane offset `lo` floats.
+__device__ __forceinline__ vecf ld_in(const float* rowp, int lo) {
+#if HEAT_TB_CHAIN
+  // Chained passes read rows a neighbour unit (possibly on another XCD)
+  // wrote in this launch: sc1 loads (HEAT_TB_CHAIN_AUX), as the resident
+  // tiles load their ghosts, so a line this XCD's L2 kept from an earlier
+  // pass of the launch is never returned (the writer's sc1 stores and flag
+  // pair with them).
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rowp), 0, 4 * V * 64,
+                                                                      0x00020000);
+  return __builtin_bit_cast(vecf, __builtin_amdgcn_raw_buffer_load_b128(rs, int(4 * lo), 0, HEAT_TB_CHAIN_AUX));
+#elif HEAT_TB_NTLOAD
+  return __builtin_nontemporal_load(reinterpret_cast<const vecf*>(rowp + lo));
 #else
-  return *reinterpret_cast<const vecf*>(p);
+  return *reinterpret_cast<const vecf*>(rowp + lo);
 #endif
 }
 
@@ -306,7 +316,7 @@ struct TbStream {
       return x;
     } else {
       if (cached_rows) row = seq0 + (row & 3);  // diagnostics: cache-resident input
-      return ld_in(src + row * pitch + lo);
+      return ld_in(src + row * pitch, lo);
     }
   }
 
@@ -421,7 +431,7 @@ struct TbStream {
       vecf c = P[U];
       {
         const int64_t nxt = min(i + RING, last_in);
-        P[U] = ld_in(src + nxt * pitch + lo);
+        P[U] = ld_in(src + nxt * pitch, lo);
       }
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -480,7 +490,7 @@ struct TbStream {
                                         int64_t* roff, int64_t* woff) {
     // Row t + 3 into the slot of row t - 3 (level 1 now reads t-2 .. t).
     if constexpr (FAST && ROLE != 2) {
-      L0[modn<6>(T6 + 3)] = ld_in(src + *roff + lo);
+      L0[modn<6>(T6 + 3)] = ld_in(src + *roff, lo);
       *roff += pitch;
     } else {
       L0[modn<6>(T6 + 3)] = load_row(src, FAST ? i + 3 : min(i + 3, last_in), pitch);

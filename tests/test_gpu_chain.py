@@ -75,3 +75,19 @@ def test_chain_with_checks_converges_alike(gpu):
     on2, off2 = _run(cfg2, True), _run(cfg2, False)
     assert on2[0].chained_passes > 0
     _same(on2, off2)
+
+
+def test_chain_l2_sized_plate_stale_lines(gpu, monkeypatch):
+    # a chained unit reads rows another unit (maybe on another
+    # XCD) wrote in the same launch; the smallest plate the chained
+    # level-split passes run on (2048 x 8192, 64 MB: 72 strip-rows per SIMD,
+    # the split pipelines' threshold; resident spans off) with the streaming
+    # build forced and 24 passes per launch, where lines an XCD's L2 kept
+    # from an earlier pass are most likely to be hit.  The chain build's row
+    # loads are sc1 now (tb_stream.inl ld_in).
+    monkeypatch.setenv("HEAT_TB_RESIDENT", "0")
+    cfg = HeatConfig(nx=2048, ny=8192, steps=24 * 12, init="random", seed=13, backend="hip",
+                     device=0)
+    on = _run(cfg, True, nt=1)
+    assert on[0].chained_passes > 0
+    _same(on, _run(cfg, False, nt=1))
