@@ -261,3 +261,40 @@ def test_cli_reference_lines_match(tmp_path, args):
             assert a["hash"] == b["hash"] and a["step"] == b["step"]
         else:
             assert v == outs["python"][1][k], k
+
+
+def test_plan_halo_rule_matches_the_model(tmp_path):
+    # The native rule (plan.hpp resident_halo_passes + resident_fits_static,
+    # what `heat --plan` prints) and its Python mirror in parallel/model.py
+    # agree on the halo depth and resident fit over plate sizes and rank
+    # counts, remainders included.
+    from parallel_heat_amd.parallel.model import (RES_MIN_PASSES, resident_fits,
+                                                  resident_halo_passes)
+    for n in (3000, 5000, 8192, 10000):
+        for g in (2, 3, 4, 6, 8):
+            for decomp in ("rows", "auto"):
+                p = json.loads(heat(["--nx", str(n), "--ny", str(n + 100), "--gpus", str(g),
+                                     "--decomp", decomp, "--plan"], tmp_path).stdout)
+                px, py = map(int, p["process_grid"].split("x"))
+                rm = resident_halo_passes(n, n + 100, px, py)
+                m = rm if rm >= RES_MIN_PASSES else 8
+                assert p["halo_passes"] == m, (n, g, decomp, p, rm)
+                # Resident iff every rank's span box at m fits (model mirror).
+                rows = [n // px + (1 if i < n % px else 0) for i in range(px)]
+                cols = [(n + 100) // py + (1 if j < (n + 100) % py else 0) for j in range(py)]
+                gr, gc = (m - 1) * 12 if px > 1 else 0, ((m - 1) * 12) // 4 * 4 if py > 1 else 0
+                fits = all(resident_fits(r + gr * ((i > 0) + (i < px - 1)),
+                                         c + gc * ((j > 0) + (j < py - 1)))
+                           for i, r in enumerate(rows) for j, c in enumerate(cols))
+                assert p["resident"] == fits, (n, g, decomp, p)
+
+
+def test_cli_warmup_restores_the_initial_state(tmp_path):
+    # --warmup N: N untimed steps (graph capture on GPUs), then the initial
+    # state again; the timed run's output is a cold run's, byte for byte.
+    base = ["--backend", "cpu", "--nx", "50", "--ny", "40", "--steps", "33", "--init", "random",
+            "--seed", "4", "--out-format", "checksum", "--json"]
+    a = heat(base + ["--out", "a.json", "--warmup", "20"], tmp_path)
+    heat(base + ["--out", "b.json"], tmp_path)
+    assert json.loads(a.stdout.splitlines()[-1])["steps_done"] == 33
+    assert (tmp_path / "a.json").read_text() == (tmp_path / "b.json").read_text()

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Counter passes of the resident tiles on the 8-GPU rank plate (1024 x 8192,
+# bench.py's whole solver) for two engine builds: the default library and
+# LIB2 (round 6: the per-wave readiness build, profiles/r6_resident_protocol.md).
+# Each pass is its own rocprofv3 run (kernel trace + counters only).
+#   bash tools/pmc_resident_ab.sh build/ab/libheat_perwave.so
+# Output: gpurun_out/pmc_res/<lib>/p<pass>/...csv
+set -o pipefail
+cd "$(dirname "$0")/.."
+R=$PWD
+LIB2=${1:?usage: pmc_resident_ab.sh LIB2}
+export TMPDIR=/tmp
+OUT=$R/gpurun_out/pmc_res
+mkdir -p "$OUT"
+cd /tmp
+for lib in default alt; do
+  if [[ $lib == alt ]]; then export HEAT_LIB=$R/$LIB2; else unset HEAT_LIB; fi
+  i=0
+  while read -r line; do
+    [[ -z $line ]] && continue
+    i=$((i+1))
+    d=$OUT/$lib/p$i
+    mkdir -p "$d"
+    timeout -k 10 240 rocprofv3 --pmc $line --kernel-trace --output-format csv -d "$d" -o p$i -- \
+      python3 $R/bench.py --nx 1024 --steps 2 --warmup 1 --no-verify > "$d.log" 2>&1 \
+      || { echo "$lib pass $i failed"; tail -20 "$d.log"; exit 1; }
+  done <<'PASSES'
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU
+FETCH_SIZE
+WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
+PASSES
+done
+echo "pmc passes done"
