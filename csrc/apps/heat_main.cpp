@@ -362,16 +362,19 @@ int main(int argc, char** argv) {
     // --halo-passes is given; resident_halo_passes), with the host-side
     // gfx950 resident fit: whether every rank's span box runs as one-round
     // resident tiles.
-    auto fits = [&](const Box& b) { return resident_fits_static(b, depth); };
+    auto shape = [&](const Box& b) { return resident_shape_static(b, depth); };
     int m = 1;
     if (ranks > 1) {
-      const int rm = resident_halo_passes(cart, P.nx, P.ny, depth, 8, fits);
+      const int rm = resident_halo_passes(cart, P.nx, P.ny, depth, 8, shape);
       m = P.halo_passes > 0 ? P.halo_passes : rm >= kResMinPasses ? rm : 8;
     }
     bool resident = true;
+    int res_rows = 0, res_waves = 0;
     for (int r = 0; r < ranks; ++r) {
       const Block b = make_block(cart, r, P.nx, P.ny);
-      resident = resident && fits(ranks > 1 ? span_box(cart, b, depth, m) : Box{0, b.lx, 0, b.ly});
+      const int sh = shape(ranks > 1 ? span_box(cart, b, depth, m) : Box{0, b.lx, 0, b.ly});
+      resident = resident && sh != 0;
+      if (r == 0) res_rows = sh >> 8, res_waves = sh & 255;
     }
     int64_t worst = 0, worst_rank = 0;
     for (int r = 0; r < ranks; ++r) {
@@ -392,10 +395,11 @@ int main(int argc, char** argv) {
     std::printf("{\"nx\": %lld, \"ny\": %lld, \"ranks\": %d, \"process_grid\": \"%dx%d\", "
                 "\"bytes_per_gpu\": %lld, \"gb_per_gpu\": %.3f, \"worst_rank\": %lld, "
                 "\"fits_288gb\": %s, \"tb_depth\": %d, \"halo_passes\": %d, \"halo\": %d, "
-                "\"resident\": %s}\n",
+                "\"resident\": %s, \"resident_tile\": \"%dx%d\"}\n",
                 (long long)P.nx, (long long)P.ny, ranks, cart.px, cart.py, (long long)worst,
                 double(worst) / 1e9, (long long)worst_rank, worst < int64_t(288e9 * 0.95) ? "true" : "false",
-                depth, m, depth * m, resident ? "true" : "false");
+                depth, m, depth * m, resident ? "true" : "false", resident ? res_rows : 0,
+                resident ? res_waves : 0);
     return 0;
   }
   const int world = env_i("WORLD_SIZE", 1), rank = env_i("RANK", 0);

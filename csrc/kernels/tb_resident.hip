@@ -50,6 +50,7 @@
 #include <tuple>
 
 #include "heat/common.hpp"
+#include "heat/plan.hpp"
 #include "tb_resident_kern.hpp"
 
 namespace heat::gpu::tbw {
@@ -145,6 +146,16 @@ bool tb_resident_fits(const Box& box, int depth, int variant) {
   const int64_t hmax = int64_t(pl.waves) * pl.rows - 2 * int64_t(depth);
   const int64_t n = ceil_div(box.rows(), hmax);
   return ceil_div(box.rows(), n) >= depth;
+}
+
+int tb_resident_shape(const Box& box, int depth, int variant) {
+  using namespace tbw;
+  const TbTuning tune = tb_tuning();
+  const ResPlan pl = plan_res(box, depth, res_xl(variant, tune), tune);
+  if (pl.rows == 0) return 0;
+  const int64_t hmax = int64_t(pl.waves) * pl.rows - 2 * int64_t(depth);
+  if (ceil_div(box.rows(), ceil_div(box.rows(), hmax)) < depth) return 0;
+  return res_shape(pl.rows, pl.waves);
 }
 
 void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const Box& box,

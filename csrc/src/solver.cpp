@@ -118,9 +118,13 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
   // Diagnostics: at most this many passes per resident span (a one-GPU
   // plate timed at the span length of an m-pass exchange interval).
   res_span_max_ = env_int("HEAT_TB_RES_SPAN", 0);
-  const bool res_ok = on_gpu() && tb_kernel() && T_ >= 4 && T_ % 2 == 0 && sched_ == Schedule::Sync &&
-                      !staged_ && gpu::tb_tuning().variant < 0 && res_env != 0 &&
-                      (world == 1 || ndev >= local_world || resident_force_);
+  // The halo depth below follows resident fit from global quantities only
+  // (every rank must pick the same m: its exchanges pair with its peers');
+  // whether this rank's spans then run resident also needs its own device.
+  const bool res_shape = on_gpu() && tb_kernel() && T_ >= 4 && T_ % 2 == 0 &&
+                         sched_ == Schedule::Sync && !staged_ && gpu::tb_tuning().variant < 0 &&
+                         res_env != 0;
+  const bool res_ok = res_shape && (world == 1 || ndev >= local_world || resident_force_);
   // Ghost depth H = m*T: with the Sync schedule one exchange feeds m passes,
   // each computing the still-valid part of the ghost ring redundantly.
   int m = 1;
@@ -129,19 +133,20 @@ Solver::Solver(const Params& p, std::shared_ptr<Transport> tr)
     // percent of redundant ghost compute for fewer exchanges, whose
     // latency dominates on small blocks (profiles/halo_passes_r1.md).
     // Unless set, m is resident-aware: when the owned blocks have a
-    // one-round resident plan, the largest m <= 8 whose span boxes still
-    // have one (8192^2 on 2 x 2 ranks: m = 5, 4144-cell boxes in 20 x 16
-    // tiles, instead of m = 8 whose 4180-cell boxes ran the split
-    // pipelines at 3.9 Tcells/s per rank; resident_halo_passes).
+    // one-round resident plan, the largest m <= 8 whose span boxes keep a
+    // plan of the same tile shape (8192^2 on 2 x 2 ranks: m = 5, 4144-cell
+    // boxes in 20 x 16 tiles, not m = 8 whose 4180-cell boxes ran the split
+    // pipelines; on 8 ranks m = 7 keeps the 12 x 16 tiles, m = 8 fell to
+    // 14 x 8 ones, -10 % per owned cell; resident_halo_passes, plan.hpp).
     // A span of m passes pays one whole-tile load and store (what a per-pass
     // tile launch pays every pass), so short spans lose their edge: below
     // kResMinPasses the split pipelines at m = 8 are kept.
     m = P_.halo_passes > 0 ? P_.halo_passes : (on_gpu() ? env_int("HEAT_HALO_PASSES", 0) : 1);
     if (m <= 0) {
       m = 8;
-      if (res_ok) {
+      if (res_shape) {
         const int rm = resident_halo_passes(cart_, P_.nx, P_.ny, T_, 8, [&](const Box& b) {
-          return gpu::tb_resident_fits(b, T_);
+          return gpu::tb_resident_shape(b, T_);
         });
         if (rm >= kResMinPasses) m = rm;
       }

@@ -133,40 +133,62 @@ Box span_box(const Cart& cart, const Block& b, int depth, int m) {
 }
 
 int resident_halo_passes(const Cart& cart, int64_t nx, int64_t ny, int depth, int mmax,
-                         const std::function<bool(const Box&)>& fits) {
+                         const std::function<int(const Box&)>& shape) {
   if (cart.world < 2 || depth < 1) return 0;
   std::vector<Block> blocks;
+  std::vector<int> own;
   int64_t min_ext = INT64_MAX;
   for (int r = 0; r < cart.world; ++r) {
     blocks.push_back(make_block(cart, r, nx, ny));
     const Block& b = blocks.back();
-    if (!fits(Box{0, b.lx, 0, b.ly})) return 0;
+    own.push_back(shape(Box{0, b.lx, 0, b.ly}));
+    if (own.back() == 0) return 0;
     if (cart.px > 1) min_ext = std::min(min_ext, b.lx);
     if (cart.py > 1) min_ext = std::min(min_ext, b.ly);
   }
   for (int m = int(std::min<int64_t>(mmax, min_ext / depth)); m >= 2; --m) {
     bool ok = true;
-    for (const Block& b : blocks) ok = ok && fits(span_box(cart, b, depth, m));
+    for (size_t i = 0; i < blocks.size() && ok; ++i)
+      ok = shape(span_box(cart, blocks[i], depth, m)) == own[i];
     if (ok) return m;
   }
   return 0;
 }
 
-bool resident_fits_static(const Box& box, int depth, int cus) {
-  // (rows per wave, waves per workgroup, workgroups per CU).
+int resident_shape_static(const Box& box, int depth, int cus) {
+  // (rows per wave, waves per workgroup, workgroups per CU), plan_res's order.
   static constexpr int kShapes[][3] = {{12, 8, 2}, {13, 8, 2}, {14, 8, 2}, {16, 8, 2},
                                        {20, 8, 1}, {24, 8, 1}, {12, 16, 1}, {20, 16, 1}};
-  if (box.empty() || depth < 4 || depth % 2 != 0 || box.c0 % 4 != 0) return false;
+  if (box.empty() || depth < 4 || depth % 2 != 0 || box.c0 % 4 != 0) return 0;
   const int64_t W = 256 - 2 * round_up(int64_t(depth), 4);
+  // tb_tile.hpp tile_step_estimate: waves per SIMD of the busiest CU x rows.
+  auto estimate = [&](int64_t units, int occ, int rows, int waves) {
+    const int64_t cap = int64_t(cus) * occ, full = (units - 1) / cap;
+    const int64_t busiest = (units - full * cap + cus - 1) / cus;
+    auto cost = [&](int64_t tiles) {
+      const double wps = double(tiles * waves) / 4.0;
+      return wps * rows * (wps >= 4.0 ? 2.7 : 3.1);
+    };
+    return double(full) * cost(occ) + cost(busiest);
+  };
+  int best = 0;
+  double best_est = 0.0;
+  int64_t best_hmax = 0;
   for (const auto& s : kShapes) {
     const int64_t hmax = int64_t(s[0]) * s[1] - 2 * int64_t(depth);
     if (hmax < std::max(depth, 4)) continue;
-    const int64_t chunks = ceil_div(box.rows(), hmax);
-    if (ceil_div(box.cols(), W) * chunks <= int64_t(cus) * s[2] &&
-        ceil_div(box.rows(), chunks) >= depth)
-      return true;
+    const int64_t units = ceil_div(box.cols(), W) * ceil_div(box.rows(), hmax);
+    if (units > int64_t(cus) * s[2]) continue;
+    const double est = estimate(units, s[2], s[0], s[1]);
+    if (best == 0 || est < best_est) {
+      best = res_shape(s[0], s[1]);
+      best_est = est;
+      best_hmax = hmax;
+    }
   }
-  return false;
+  // tb_resident_fits: every tile but the last of a strip at least K rows.
+  if (best != 0 && ceil_div(box.rows(), ceil_div(box.rows(), best_hmax)) < depth) return 0;
+  return best;
 }
 
 }  // namespace heat

@@ -46,18 +46,21 @@ XGMI = {
     "allreduce_us": 12.0,        # one 4-byte ncclAllReduce(max) per check
 }
 
-# Whole-solver rate (Tcells/s of owned cells) of one MI355X on a bench plate
-# (plate edges top and bottom) vs strip-rows per SIMD of that plate (232
-# useful columns per 256-column strip at depth 12, 1024 SIMDs), in two
-# families: spans whose box has a one-dispatch-round resident plan (every
-# tile co-resident for all passes between exchanges, tb_resident.hip) and
-# the rest (level-split pipelines / per-pass tiles).  Round 5 measurements,
-# enqueued bench steps (profiles/r5_raw/r5h_*.txt, r5f_b*.txt, r5c_b1192.txt).
+# Whole-solver rate (Tcells/s) of one MI355X on a bench plate (plate edges
+# top and bottom) vs strip-rows per SIMD of that plate (232 useful columns
+# per 256-column strip at depth 12, 1024 SIMDs), in two families: spans whose
+# box has a one-dispatch-round resident plan (every tile co-resident for all
+# passes between exchanges, tb_resident.hip) and the rest (level-split
+# pipelines / per-pass tiles).  Resident points are long-span rates of the
+# span BOX (multi-rank spans pay SPAN_COST below); the rest are rates of the
+# owned block.  Enqueued bench steps, rounds 5-6 (profiles/r5_raw/r5h_*.txt,
+# r5f_b*.txt, profiles/r6_raw/r6d/, r6f/).
 RESIDENT_POINTS: List[tuple] = [
     (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
-    (36.0, 4.03),   # 1024 x 8192 3.96 / 2048 x 4096 4.10 (8 GPUs): 12 x 16 tiles
-    (42.0, 4.29),   # 1192 x 8192 (the 1-D 8-GPU middle rank's first box): 14 x 8
-    (72.0, 5.29),   # 2048 x 8192 5.25-5.34 / 4096 x 4096 5.22-5.34 (4 GPUs): 20 x 16
+    (36.0, 4.16),   # 1024 x 8192 (12 x 16 tiles, 7 chunks of 146 rows: 87 % filled)
+    (39.0, 4.65),   # 1120 x 8192 at 5-pass spans 4.08, 2192 x 4168 at 7 4.23 (12 x 16)
+    (41.0, 4.67),   # 1168 x 8192 at 7-pass spans 4.24 (12 x 16, 7 full chunks)
+    (72.0, 5.30),   # 2048 x 8192 5.25-5.34 / 4096^2 5.22-5.34 / 4144^2 5.37 (20 x 16)
 ]
 STREAM_POINTS: List[tuple] = [
     (18.0, 3.0),    # extrapolated, unmeasured
@@ -86,17 +89,44 @@ RES_SHAPES = [(12, 8, 2), (13, 8, 2), (14, 8, 2), (16, 8, 2), (20, 8, 1), (24, 8
               (12, 16, 1), (20, 16, 1)]
 
 
-def resident_fits(rows: int, cols: int, depth: int = 12) -> bool:
-    """A rows x cols box has a one-round resident plan (all tiles co-resident)."""
+def _tile_step_estimate(units: int, occ: int, rows: int, waves: int) -> float:
+    """csrc/kernels/tb_tile.hpp tile_step_estimate (the planner's choice)."""
+    cap = CUS * occ
+    full = (units - 1) // cap
+    busiest = (units - full * cap + CUS - 1) // CUS
+
+    def cost(tiles):
+        wps = tiles * waves / 4.0
+        return wps * rows * (2.7 if wps >= 4.0 else 3.1)
+    return full * cost(occ) + cost(busiest)
+
+
+def resident_shape(rows: int, cols: int, depth: int = 12) -> tuple:
+    """The resident planner's (rows per wave, waves) for a rows x cols box, or
+    None without a one-round plan (csrc/src/topology.cpp
+    resident_shape_static, tb_resident.hip plan_res)."""
+    if rows <= 0 or cols <= 0 or depth < 4 or depth % 2:
+        return None
     strips = math.ceil(cols / (256 - 2 * ((depth + 3) // 4 * 4)))
+    best, best_est, best_h = None, 0.0, 0
     for r, nw, occ in RES_SHAPES:
         h = r * nw - 2 * depth
         if h < max(depth, 4):
             continue
-        chunks = math.ceil(rows / h)
-        if strips * chunks <= CUS * occ and math.ceil(rows / chunks) >= depth:
-            return True
-    return False
+        units = strips * math.ceil(rows / h)
+        if units > CUS * occ:
+            continue
+        est = _tile_step_estimate(units, occ, r, nw)
+        if best is None or est < best_est:
+            best, best_est, best_h = (r, nw), est, h
+    if best is not None and math.ceil(rows / math.ceil(rows / best_h)) < depth:
+        return None
+    return best
+
+
+def resident_fits(rows: int, cols: int, depth: int = 12) -> bool:
+    """A rows x cols box has a one-round resident plan (all tiles co-resident)."""
+    return resident_shape(rows, cols, depth) is not None
 
 
 RES_MIN_PASSES = 4  # csrc/include/heat/plan.hpp kResMinPasses
@@ -112,12 +142,14 @@ def resident_halo_passes(nx: int, ny: int, px: int, py: int, depth: int = 12,
     """The solver's resident-aware passes per exchange (topology.cpp
     resident_halo_passes): the largest m in [2, mmax] for which every rank's
     first span box -- the owned block grown by (m - 1) * depth on each side
-    with a neighbour -- has a one-round resident plan; 0 if the owned blocks
-    have none or no m does.  The solver keeps m = 8 below RES_MIN_PASSES."""
+    with a neighbour -- has a one-round resident plan of the same tile shape
+    as its owned block's; 0 if the owned blocks have none or no m keeps it.
+    The solver keeps m = 8 below RES_MIN_PASSES."""
     if px * py < 2:
         return 0
     rows, cols = _blocks(nx, px), _blocks(ny, py)
-    if not all(resident_fits(r, c, depth) for r in rows for c in cols):
+    own = {(r, c): resident_shape(r, c, depth) for r in rows for c in cols}
+    if any(v is None for v in own.values()):
         return 0
     ext = min((rows if px > 1 else []) + (cols if py > 1 else []))
     for m in range(min(mmax, ext // depth), 1, -1):
@@ -128,7 +160,7 @@ def resident_halo_passes(nx: int, ny: int, px: int, py: int, depth: int = 12,
             for j, c in enumerate(cols):
                 er = gr * ((i > 0) + (i < px - 1))
                 ec = gc * ((j > 0) + (j < py - 1))
-                ok = ok and resident_fits(r + er, c + ec, depth)
+                ok = ok and resident_shape(r + er, c + ec, depth) == own[(r, c)]
         if ok:
             return m
     return 0
@@ -247,9 +279,13 @@ def predict(cfg: HeatConfig, world: int, depth: int = 12, halo_passes: int = 8,
     ext_r = (2 if px > 2 else 1) * (H - depth) if px > 1 else 0
     ext_c = (2 if py > 2 else 1) * (H - depth) if py > 1 else 0
     resident = schedule == "sync" and resident_fits(lx + ext_r, ly + ext_c, depth)
-    rate = rate_tcells(lx, ly, resident) * 1e12
-    if resident and world > 1:
-        rate /= 1.0 + SPAN_COST / m
+    if resident:
+        # The span box's long-span rate, less the span's load / store.
+        rate = rate_tcells(lx + ext_r, ly + ext_c, True) * 1e12
+        if world > 1:
+            rate /= 1.0 + SPAN_COST / m
+    else:
+        rate = rate_tcells(lx, ly, False) * 1e12
     cells = (lx + ext_r) * (ly + ext_c)
     compute_s = cells * 1000 / rate
     exchanges = math.ceil(1000 / H) if world > 1 else 0

@@ -196,11 +196,12 @@ def test_cli_plan_resident_aware_halo(tmp_path):
     # Passes per exchange follow resident fit (plan.hpp resident_halo_passes,
     # the same rule as the solver and parallel/model.py): 8192^2 on 2 x 2
     # ranks takes m = 5 (4144-cell span boxes, 20 x 16 resident tiles) instead
-    # of m = 8 (4180: no one-round plan); slabs whose only fitting m is below
+    # of m = 8 (4180: no one-round plan); 8 ranks take m = 7 (m = 8 boxes fall
+    # to another tile shape); slabs whose only fitting m is below
     # kResMinPasses keep m = 8; --halo-passes overrides.
     from parallel_heat_amd.parallel.model import resident_halo_passes
-    want = {("auto", 4): (5, True), ("rows", 4): (8, False), ("auto", 8): (8, True),
-            ("rows", 8): (8, True), ("auto", 2): (8, False)}
+    want = {("auto", 4): (5, True), ("rows", 4): (8, False), ("auto", 8): (7, True),
+            ("rows", 8): (7, True), ("auto", 2): (8, False)}
     for (decomp, g), (m, res) in want.items():
         p = json.loads(heat(["--nx", "8192", "--ny", "8192", "--gpus", str(g), "--decomp", decomp,
                              "--plan"], tmp_path).stdout)
@@ -298,3 +299,23 @@ def test_cli_warmup_restores_the_initial_state(tmp_path):
     heat(base + ["--out", "b.json"], tmp_path)
     assert json.loads(a.stdout.splitlines()[-1])["steps_done"] == 33
     assert (tmp_path / "a.json").read_text() == (tmp_path / "b.json").read_text()
+
+
+def test_plan_tile_shape_matches_the_model(tmp_path):
+    # The host planner mirror (topology.cpp resident_shape_static, what
+    # `heat --plan` reports as resident_tile) and parallel/model.py's
+    # resident_shape pick the same tile shape (tb_resident.hip plan_res's
+    # lowest tile_step_estimate): 12 x 16 up to 1168 rows of 8192 columns,
+    # 14 x 8 two per CU at 1192, 20 x 16 on the 4-GPU plates.
+    from parallel_heat_amd.parallel.model import resident_shape
+    want = {(1024, 8192): (12, 16), (1168, 8192): (12, 16), (1192, 8192): (14, 8),
+            (2192, 4168): (12, 16), (2216, 4180): (14, 8), (4144, 4144): (20, 16),
+            (4180, 4180): None, (2048, 8192): (20, 16), (300, 1000): (12, 8)}
+    for (r, c), sh in want.items():
+        assert resident_shape(r, c) == sh, (r, c)
+    for r in (200, 640, 1000, 1100, 1500, 2100, 3000, 4100):
+        for c in (500, 2000, 4100, 8192):
+            p = json.loads(heat(["--nx", str(r), "--ny", str(c), "--tb-depth", "12", "--plan"],
+                                tmp_path).stdout)
+            sh = resident_shape(r, c)
+            assert p["resident_tile"] == (f"{sh[0]}x{sh[1]}" if sh else "0x0"), (r, c, p)
