@@ -32,12 +32,6 @@
 #if HEAT_TB_PACKED && HEAT_TB_V != 4
 #error "the packed row update is written for float4 lanes"
 #endif
-// Main-loop stores as buffer stores: the row's buffer resource built on the
-// scalar unit (no 64-bit VALU address per row), a store-less lane given an
-// out-of-range voffset (no exec-mask branch per row).
-#ifndef HEAT_TB_BUFSTORE
-#define HEAT_TB_BUFSTORE 0
-#endif
 // Row cache policy.  HEAT_TB_NTSTORE / HEAT_TB_NTLOAD 1: non-temporal output
 // stores / input-row loads (the streaming build tb_split_nt.hip, taken when
 // one pass sweeps more than the MALL holds: the rows a pass writes are read
@@ -45,10 +39,8 @@
 // 5.03-5.09 -> 5.24-5.25 Tcells/s, 131072^2 5.53 -> 5.63; but the 4096 x
 // 8192 plate (134 MB, inside the MALL) 4.76-4.83 -> 4.66-4.70, so the
 // smaller fields keep the plain build (profiles/r5_stores.md).
-// Experiment builds (HEAT_LIB A/B): HEAT_TB_STORE_AUX = the cache-policy
-// bits of the buffer-store build (HEAT_TB_BUFSTORE); HEAT_TB_DIAG_FIXEDSTORE
-// 1 = every store of a unit to one row (the store instructions without the
-// HBM write stream; timing only, wrong results).
+// (Round 5's buffer-store and fixed-row-store experiment builds,
+// profiles/r5_stores.md, were removed in round 6.)
 #ifndef HEAT_TB_NTSTORE
 #define HEAT_TB_NTSTORE 0
 #endif
@@ -63,27 +55,12 @@
 #ifndef HEAT_TB_CHAIN_AUX
 #define HEAT_TB_CHAIN_AUX 16
 #endif
-// s_sleep argument between a chained unit's flag polls; HEAT_TB_CHAIN_NOWAIT
-// 1 (diagnostics, wrong results) skips the waits.
+// s_sleep argument between a chained unit's flag polls.
 #ifndef HEAT_TB_CHAIN_SLEEP
 #define HEAT_TB_CHAIN_SLEEP 1
 #endif
-#ifndef HEAT_TB_CHAIN_NOWAIT
-#define HEAT_TB_CHAIN_NOWAIT 0
-#endif
-// Diagnostics: the chained build with the streaming build's non-temporal
-// stores (not write-through: valid only with HEAT_TB_CHAIN_NOWAIT timing).
-#ifndef HEAT_TB_CHAIN_NTSTORE
-#define HEAT_TB_CHAIN_NTSTORE 0
-#endif
-#if HEAT_TB_CHAIN && (HEAT_TB_V != 4 || HEAT_TB_BUFSTORE)
+#if HEAT_TB_CHAIN && HEAT_TB_V != 4
 #error "the chained build stores float4 rows through buffer stores of its own"
-#endif
-#ifndef HEAT_TB_STORE_AUX
-#define HEAT_TB_STORE_AUX 0
-#endif
-#ifndef HEAT_TB_DIAG_FIXEDSTORE
-#define HEAT_TB_DIAG_FIXEDSTORE 0
 #endif
 
 namespace heat::gpu::HEAT_TB_NS {
@@ -278,7 +255,6 @@ struct TbStream {
   // and the row arithmetic stays on the scalar unit.
   int lo = 0;
   bool nostore = false;  // diagnostics only (kTbDiagNoStore): timing without the stores
-  int vso = 0;  // HEAT_TB_BUFSTORE: this lane's store voffset (out of range: no store)
   bool cached_rows = false;  // diagnostics only (kTbDiagCachedRows): loads hit 4 rows
 
   // Level-split pipeline state (ROLE 1/2): a ring of kSplitRing rows of the
@@ -348,34 +324,8 @@ struct TbStream {
       off = *woff;
       *woff += pitch;
     }
-#if HEAT_TB_BUFSTORE
-    if constexpr (FAST) {
-      typedef unsigned uvec __attribute__((ext_vector_type(V)));
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + off, 0, 4 * V * 64, 0x00020000);
-#if HEAT_TB_V == 4
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uvec, out), rs, vso, 0, HEAT_TB_STORE_AUX);
-#else
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec, out), rs, vso, 0, HEAT_TB_STORE_AUX);
-#endif
-      if constexpr (LASTRES) {
-        float d[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) d[j] = (store_lane && (j == 0 || rc > j)) ? __builtin_fabsf(out[j] - b[j]) : 0.f;
-#pragma unroll
-        for (int j = 0; j < V; j += 2)
-          m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(d[j], d[j + 1]));
-      }
-      return;
-    }
-#endif
     if ((FAST || (ro >= rb && ro < re)) && store_lane) {
-#if HEAT_TB_DIAG_FIXEDSTORE
-      // Diagnostics build: every store of the unit goes to its first output
-      // row (same instructions, L2-resident target: the store issue cost
-      // without the HBM write traffic; wrong results).
-      off = rb * pitch;
-#endif
-#if HEAT_TB_CHAIN && !HEAT_TB_CHAIN_NTSTORE
+#if HEAT_TB_CHAIN
       // Chained passes: write-through (sc1) 16-B stores, so a neighbour
       // unit on another XCD reads them after this unit's flag (drained
       // stores, then an sc1 flag store; tb_chain_kernel).
@@ -766,7 +716,6 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.qrb = int(rb);
       st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
-      st.vso = store_lane && !st.nostore ? 4 * V * lane : int(0x80000000u);
       st.cached_rows = a.flags & tbdetail::kTbDiagCachedRows;
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
@@ -796,7 +745,6 @@ __device__ __forceinline__ float tb_segment(const TbArgs& a, const TbBox& bx, in
       st.qrb = int(rb);
       st.qlen = int(re - rb);
       st.nostore = a.flags & tbdetail::kTbDiagNoStore;
-      st.vso = store_lane && !st.nostore ? 4 * V * lane : int(0x80000000u);
       st.run(src, dst, pitch, rb, re, rlo, rhi, store_lane, upd);
       m = st.m;
     }
@@ -1065,7 +1013,7 @@ __global__ __launch_bounds__(256, (tb_split_waves_per_simd<K, K1>())) void tb_ch
     float* dst = a.dst;
     int64_t qoff = 0;
     for (int p = 0; p < c.passes; ++p) {
-      if (stage == 0 && p > 0 && !HEAT_TB_CHAIN_NOWAIT) {
+      if (stage == 0 && p > 0) {
         for (unsigned spins = 0;; ++spins) {
           const unsigned v =
               nf >= 0 ? __hip_atomic_load(c.flags + nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
