@@ -211,6 +211,8 @@ int heat_op_residual(const float* a, const float* b, int64_t pitch, int64_t r0, 
 int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows, int* hx,
                 int* hy);
 int heat_tb_supported(int depth);
+/* 1 once libheat_exp.so (the experiment kernels, `make exp`) has registered them. */
+int heat_tb_exp_loaded(void);
 
 #ifdef __cplusplus
 }

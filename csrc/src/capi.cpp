@@ -163,6 +163,10 @@ heat::gpu::StencilGeom geom(int64_t pitch, int64_t gx0, int64_t gy0, int64_t nx,
 }
 }  // namespace
 
+namespace heat::gpu {
+bool tb_exp_loaded();  // stencil.hip (kernels/tb_exp.hpp)
+}  // namespace heat::gpu
+
 extern "C" {
 
 const char* heat_last_error(void) { return g_err.c_str(); }
@@ -563,6 +567,8 @@ int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows,
 }
 
 int heat_tb_supported(int depth) { return heat::gpu::tb_depth_supported(depth) ? 1 : 0; }
+
+int heat_tb_exp_loaded(void) { return heat::gpu::tb_exp_loaded() ? 1 : 0; }
 
 int heat_tb_mid_residual(int depth) { return heat::gpu::tb_mid_residual(depth) ? 1 : 0; }
 

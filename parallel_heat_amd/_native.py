@@ -183,6 +183,7 @@ _SIGS = {
     "heat_layout": (c_int, [c_int64, c_int64, c_int, POINTER(c_int64), POINTER(c_int64),
                             POINTER(c_int), POINTER(c_int)]),
     "heat_tb_supported": (c_int, [c_int]),
+    "heat_tb_exp_loaded": (c_int, []),
     "heat_tb_mid_residual": (c_int, [c_int]),
     "heat_group_transport": (c_int, [ctypes.c_char_p, c_int, POINTER(c_int32), POINTER(c_int32)]),
     "heat_solver_abort": (c_int, [c_void_p]),
