@@ -224,7 +224,11 @@ def lib():
             raise NativeError(f"{LIB_PATH} is missing and could not be built")
         L = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
+            # An older build (HEAT_LIB A/Bs) may lack a newer entry point: it
+            # stays unbound, and only calling it fails.
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         if L.heat_abi_version() != ABI_VERSION:
