@@ -213,6 +213,10 @@ int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows,
 int heat_tb_supported(int depth);
 /* 1 once libheat_exp.so (the experiment kernels, `make exp`) has registered them. */
 int heat_tb_exp_loaded(void);
+/* The resident tile plan of a rows x cols box at `depth` as rows << 8 | waves
+   (0: none): the device planner (device = 1, needs a GPU) or its host mirror
+   (device = 0, what `heat --plan` uses). */
+int heat_resident_shape(int64_t rows, int64_t cols, int depth, int device, int32_t* shape);
 
 #ifdef __cplusplus
 }

@@ -561,12 +561,14 @@ void tb_step(const float* src, float* dst, const StencilGeom& g, const Box* boxe
              variant);
   if (variant & tbv::kTile) {
     // The tile kernel runs steps in (down, up) pairs: even depths only; an
-    // odd pass (a remainder or a check-cut pass) streams.
+    // odd pass (a remainder or a check-cut pass) streams, with the default
+    // single-wave build (scalar update + ramp; dropping only the tile bits
+    // left the packed build, an experiment kernel since round 6).
     if (depth % 2 == 0) {
       tbw::step(src, dst, g, boxes, nbox, depth, resid, res_level, st, variant, tune);
       return;
     }
-    variant &= ~(tbv::kTile | tbv::kTileDpp);
+    variant = (variant & ~(tbv::kTile | tbv::kTileDpp | 3)) | tbv::kDefault;
   }
   // Inner-level residuals: the level-split build at depth 12 (and the tiles).
   HEAT_CHECK(res_level == 0 || (tb_variant_split(variant) && depth == kTbDeepDepth),

@@ -1,5 +1,6 @@
 // C ABI (see capi.h).
 #include "heat/capi.h"
+#include "heat/plan.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -569,6 +570,13 @@ int heat_layout(int64_t lx, int64_t ly, int halo, int64_t* pitch, int64_t* rows,
 int heat_tb_supported(int depth) { return heat::gpu::tb_depth_supported(depth) ? 1 : 0; }
 
 int heat_tb_exp_loaded(void) { return heat::gpu::tb_exp_loaded() ? 1 : 0; }
+
+int heat_resident_shape(int64_t rows, int64_t cols, int depth, int device, int32_t* shape) {
+  return guard([&] {
+    const heat::Box b{0, rows, 0, cols};
+    *shape = device ? heat::gpu::tb_resident_shape(b, depth) : heat::resident_shape_static(b, depth);
+  });
+}
 
 int heat_tb_mid_residual(int depth) { return heat::gpu::tb_mid_residual(depth) ? 1 : 0; }
 

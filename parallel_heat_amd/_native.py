@@ -184,6 +184,8 @@ _SIGS = {
                             POINTER(c_int), POINTER(c_int)]),
     "heat_tb_supported": (c_int, [c_int]),
     "heat_tb_exp_loaded": (c_int, []),
+    "heat_register_exp_kernels": (None, [c_void_p]),
+    "heat_resident_shape": (c_int, [c_int64, c_int64, c_int, c_int, POINTER(c_int32)]),
     "heat_tb_mid_residual": (c_int, [c_int]),
     "heat_group_transport": (c_int, [ctypes.c_char_p, c_int, POINTER(c_int32), POINTER(c_int32)]),
     "heat_solver_abort": (c_int, [c_void_p]),
@@ -257,7 +259,15 @@ def load_exp():
             if not EXP_PATH.exists():
                 raise NativeError(f"{EXP_PATH} is missing: build it with `make exp`")
             _exp = ctypes.CDLL(str(EXP_PATH))
+        _exp.heat_exp_register()  # (again, after an unload_exp())
     return _exp
+
+
+def unload_exp() -> None:
+    """Unregister the experiment kernels (the library stays mapped): launches
+    that need one fail again, as in a process that never loaded them."""
+    L = lib()
+    L.heat_register_exp_kernels(None)
 
 
 def available() -> bool:
@@ -305,5 +315,5 @@ __all__ = [
     "HeatParams", "HeatComm", "HeatMsg", "HeatTransportInfo", "HeatTbTuning", "HeatRunStats", "HeatBlockInfo", "HeatChecksum",
     "SENDRECV_CB", "ALLREDUCE_CB", "BARRIER_CB", "NativeError", "lib", "call", "check",
     "available", "build_native", "loaded_path", "device_count", "rccl_unique_id",
-    "require_gpu_native", "LIB_PATH", "CLI_PATH", "c_uint", "EXP_PATH", "load_exp",
+    "require_gpu_native", "LIB_PATH", "CLI_PATH", "c_uint", "EXP_PATH", "load_exp", "unload_exp",
 ]

@@ -35,4 +35,7 @@ def exp_kernels():
     cover the measured-slower TB builds (packed, float2, mixed shifts,
     chained passes) load them; the product library does not carry them."""
     from parallel_heat_amd import _native
-    return _native.load_exp()
+    yield _native.load_exp()
+    # Unregistered again: the product-path tests of later modules must not
+    # lean on them (an odd-depth tile pass did, until round 6).
+    _native.unload_exp()

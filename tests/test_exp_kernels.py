@@ -29,13 +29,15 @@ def test_product_library_carries_no_experiment_kernels():
 def test_exp_library_registers_when_loaded():
     # A fresh interpreter: nothing registered until load_exp().
     code = ("from parallel_heat_amd import _native as n; a = n.lib().heat_tb_exp_loaded(); "
-            "n.load_exp(); print(a, n.lib().heat_tb_exp_loaded())")
+            "n.load_exp(); b = n.lib().heat_tb_exp_loaded(); n.unload_exp(); "
+            "c = n.lib().heat_tb_exp_loaded(); n.load_exp(); "
+            "print(a, b, c, n.lib().heat_tb_exp_loaded())")
     env = dict(os.environ, PYTHONPATH=str(_native.REPO_DIR))
     env.pop("HEAT_EXP", None)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
-    assert out.stdout.split() == ["0", "1"]
+    assert out.stdout.split() == ["0", "1", "0", "1"]
     out = subprocess.run([sys.executable, "-c", "from parallel_heat_amd import _native as n; "
                           "print(n.lib().heat_tb_exp_loaded())"], capture_output=True, text=True,
                          env=dict(env, HEAT_EXP="1"), timeout=300)

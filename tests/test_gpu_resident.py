@@ -198,3 +198,21 @@ def test_resident_inner_checks_not_converging(gpu, monkeypatch, interval):
     assert not r1[0].converged and r1[0].checks == r0[0].checks == 600 // interval
     assert np.float32(r1[0].last_resid) == np.float32(r0[0].last_resid)
     assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+
+
+def test_resident_shape_host_mirror_matches_the_device(gpu):
+    # `heat --plan` and parallel/model.py plan resident tiles without a GPU
+    # (topology.cpp resident_shape_static: the planner's shapes with gfx950's
+    # co-resident workgroups per CU written in); the solver asks the device
+    # planner (gpu::tb_resident_shape: the occupancy API).  Same answers.
+    import ctypes
+
+    from parallel_heat_amd import _native
+    for r in (40, 203, 640, 1024, 1096, 1168, 1192, 1500, 2048, 2120, 2192, 2216, 3000, 4144, 4180):
+        for c in (70, 517, 2000, 4096, 4168, 4180, 8192):
+            got = []
+            for dev in (1, 0):
+                v = ctypes.c_int32()
+                _native.call("heat_resident_shape", r, c, 12, dev, ctypes.byref(v))
+                got.append(v.value)
+            assert got[0] == got[1], (r, c, [(g >> 8, g & 255) for g in got])
