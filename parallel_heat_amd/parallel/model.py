@@ -57,9 +57,9 @@ XGMI = {
 # r5f_b*.txt, profiles/r6_raw/r6d/, r6f/).
 RESIDENT_POINTS: List[tuple] = [
     (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
-    (36.0, 4.16),   # 1024 x 8192 (12 x 16 tiles, 7 chunks of 146 rows: 87 % filled)
-    (39.0, 4.65),   # 1120 x 8192 at 5-pass spans 4.08, 2192 x 4168 at 7 4.23 (12 x 16)
-    (41.0, 4.67),   # 1168 x 8192 at 7-pass spans 4.24 (12 x 16, 7 full chunks)
+    (36.0, 4.36),   # 1024 x 8192 4.32-4.36 / 2048 x 4096 4.39 (12 x 16 tiles, DPP shifts, r6i)
+    (38.5, 4.81),   # 2192 x 4168 (the 4 x 2 8-GPU box at m = 7): 4.38 at 7-pass spans
+    (41.0, 5.14),   # 1168 x 8192 (the 8 x 1 8-GPU box at m = 7, 7 full chunks): 4.67 at 7
     (72.0, 5.30),   # 2048 x 8192 5.25-5.34 / 4096^2 5.22-5.34 / 4144^2 5.37 (20 x 16)
 ]
 STREAM_POINTS: List[tuple] = [
