@@ -1,20 +1,24 @@
 #!/bin/bash
 # Counter passes of the resident tiles on the 8-GPU rank plate (1024 x 8192,
-# bench.py's whole solver) for two engine builds: the default library and
-# LIB2 (round 6: the per-wave readiness build, profiles/r6_resident_protocol.md).
-# Each pass is its own rocprofv3 run (kernel trace + counters only).
-#   bash tools/pmc_resident_ab.sh build/ab/libheat_perwave.so
-# Output: gpurun_out/pmc_res/<lib>/p<pass>/...csv
+# bench.py's whole solver) for the default and an alternative: another
+# engine build (LIB2, a path: round 6's per-wave readiness build) or an
+# environment setting (VAR=value, e.g. HEAT_TB_TILE_XL=2: round 5's lane
+# shifts).  Each pass is its own rocprofv3 run (kernel trace + counters only).
+#   bash tools/pmc_resident_ab.sh build/ab/libheat_perwave.so [OUTDIR]
+#   bash tools/pmc_resident_ab.sh HEAT_TB_TILE_XL=2 pmc_xl
+# Output: gpurun_out/<OUTDIR, default pmc_res>/{default,alt}/p<pass>/...csv
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$PWD
-LIB2=${1:?usage: pmc_resident_ab.sh LIB2}
+ALT=${1:?usage: pmc_resident_ab.sh LIB2|VAR=value [OUTDIR]}
 export TMPDIR=/tmp
-OUT=$R/gpurun_out/pmc_res
+OUT=$R/gpurun_out/${2:-pmc_res}
 mkdir -p "$OUT"
 cd /tmp
 for lib in default alt; do
-  if [[ $lib == alt ]]; then export HEAT_LIB=$R/$LIB2; else unset HEAT_LIB; fi
+  unset HEAT_LIB
+  if [[ $lib == alt && $ALT == *=* ]]; then export "${ALT?}"
+  elif [[ $lib == alt ]]; then export HEAT_LIB=$R/$ALT; fi
   i=0
   while read -r line; do
     [[ -z $line ]] && continue
@@ -28,6 +32,7 @@ for lib in default alt; do
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU
 FETCH_SIZE
 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
+SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU SQ_INSTS_SALU GRBM_COUNT
 PASSES
 done
 echo "pmc passes done"
