@@ -21,8 +21,11 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // PK): on 12-row waves it measured +3-6 % (1024 x 8192 4.06-4.18 vs
 // 3.91-3.95, 2048 x 4096 4.17 vs 4.04, session r5j); its pair temporaries
 // spilled taller waves (20 x 16: 676 B/lane, 1.04 Tcells/s) and, next to
-// the residual code, the 12-row RES 1 builds (resident: 48 -> 200 B/lane),
-// which keep the scalar update.
+// the residual code, the 12-row RES 1 builds with ds_bpermute shifts
+// (resident XL 2: 48 -> 200 B/lane), which keep the scalar update.  The
+// RES 1 builds with DPP shifts (XL 0) take it: resident 12-row checks every
+// 20 / 50 steps ran 4.01-4.02 / 4.07 vs 3.80 / 3.83 Tcells/s (1024 x 8192,
+// session r6l; 68 B/lane, none of it in a step loop).
 constexpr int kTilePkRows = 12;
 
 // Lane l <- lane l-1 / l+1.  Lanes 0 and 63 lie in the strip overlap
@@ -311,7 +314,7 @@ struct Tile {
       const vecf outside = i == 0 ? first_nb : last_nb;
       const vecf n = r == 0 ? outside : (DOWN ? prev : u[r - 1]);
       const vecf so = r == R - 1 ? outside : (DOWN ? u[r + 1] : prev);
-      u[r] = up.template apply<(R <= kTilePkRows && RES == 0)>(n, cur, so, wl[r], er[r],
+      u[r] = up.template apply<(R <= kTilePkRows && (RES == 0 || XL == 0))>(n, cur, so, wl[r], er[r],
                                                                 (rowmask >> r) & 1u);
       if (i == 0) xc.publish(0, u[r]);
       if (i == R - 1) xc.publish(1, u[r]);
