@@ -205,9 +205,9 @@ void tb_resident_step(const float* src, float* dst, const StencilGeom& g, const 
   // (tools/probes/stencil_chain.hip: packed + DPP 65 vs 73 cycles per row
   // update; 1168 x 8192 plate 4.90 vs 4.62 Tcells/s, 2192 x 4168 4.54 vs
   // 4.43, profiles/r6_raw/r6h/; checks every 20 steps on 1024 x 8192 4.01
-  // vs 3.80, r6l; its plate-edge tiles take the generic path: edge modes
-  // built for XL 0 too made it spill).  The round-4 all-DPP build was 11 %
-  // slower with the scalar update, which the taller tiles keep.
+  // vs 3.80, r6l; unchecked launches have the left / element-3 right edge
+  // modes, tile_dispatch).  The round-4 all-DPP build was 11 % slower with
+  // the scalar update, which the taller tiles keep.
   if (variant < 0 && tune.tile_xl < 0 && pl.rows <= kTilePkRows &&
       cached_occupancy_res(pl.rows, pl.waves, 0) >= cached_occupancy_res(pl.rows, pl.waves, xl))
     xl = 0;

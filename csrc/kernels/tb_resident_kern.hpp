@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64 * NW, (tile_waves_per_simd<R, NW>())) void tile_
   const int64_t wx_lo = g.gx0 + ub - K + int64_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * R;
   const int64_t wx_hi = wx_lo + R - 1;
   const int mode = (ra.diag & 8) ? kTileGeneric : tile_mode(g, wx_lo, wx_hi, gy_lo, gy_hi, ra.diag & 16);
-  tile_dispatch<XL>(mode, [&](auto mode_c) {
+  tile_dispatch<XL, (RES == 0 && R <= kTilePkRows)>(mode, [&](auto mode_c) {
     resident_run<R, NW, decltype(mode_c)::value, XL, RES>(ra, bx, strip, t, blk, xch);
     return 0.f;
   });

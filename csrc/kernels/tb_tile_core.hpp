@@ -218,12 +218,25 @@ __device__ __forceinline__ void tile_pass_steps(int K, StepFn&& st, int acc_step
 }
 
 // Calls f(std::integral_constant<int, MODE>) for the tile's mode.  The edge
-// modes are built for the default lane shifts (XL 2) only; the others take
-// the generic path on every edge tile.
-template <int XL, class F>
+// modes are built for the mixed lane shifts (XL 2) and, for the unchecked
+// resident DPP launches (XL 0, RES 0), the left and the element-3 right
+// mode: a plate of a multiple of 4 columns whose local column 0 is global
+// column 0 mod 4 (every power-of-two grid and its rank boxes) has its last
+// column in element 3.  They cost 12 B/lane on the 12-row RES 0 kernels and
+// gained 0-3 % on the 8-GPU rank boxes (2192 x 4168 at 7-pass spans 4.40-4.51
+// vs 4.26-4.38, 2048 x 4096 4.42-4.47 vs 4.33-4.36; sessions r6o, r6p); with
+// the residual code (RES 1) they spilled 68 -> 172 B/lane.  XL0_EDGES: the
+// caller is such a launch (<= kTilePkRows rows: taller DPP builds only run
+// when forced; 20 x 16 spilled 20 B/lane with them).  Everything else takes the generic path on its
+// edge tiles.
+template <int XL, bool XL0_EDGES = false, class F>
 __device__ __forceinline__ float tile_dispatch(int mode, F&& f) {
   using std::integral_constant;
   if (mode == kTileInterior) return f(integral_constant<int, kTileInterior>{});
+  if constexpr (XL == 0 && XL0_EDGES) {
+    if (mode == kTileLeft) return f(integral_constant<int, kTileLeft>{});
+    if (mode == kTileRight + 3) return f(integral_constant<int, kTileRight + 3>{});
+  }
   if constexpr (XL == 2) {
     switch (mode) {
       case kTileLeft: return f(integral_constant<int, kTileLeft>{});
