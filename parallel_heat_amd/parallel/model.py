@@ -54,11 +54,11 @@ XGMI = {
 # pipelines / per-pass tiles).  Resident points are long-span rates of the
 # span BOX (multi-rank spans pay SPAN_COST below); the rest are rates of the
 # owned block.  Enqueued bench steps, rounds 5-6 (profiles/r5_raw/r5h_*.txt,
-# r5f_b*.txt, profiles/r6_raw/r6d/, r6f/).
+# r5f_b*.txt, profiles/r6_raw/r6d/, r6f/, r6o/ - r6q/).
 RESIDENT_POINTS: List[tuple] = [
     (18.0, 3.0),    # 512 x 8192 (16-GPU-like blocks; extrapolated, unmeasured)
-    (36.0, 4.36),   # 1024 x 8192 4.32-4.36 / 2048 x 4096 4.39 (12 x 16 tiles, DPP shifts, r6i)
-    (38.5, 4.81),   # 2192 x 4168 (the 4 x 2 8-GPU box at m = 7): 4.38 at 7-pass spans
+    (36.0, 4.40),   # 1024 x 8192 4.33-4.45 / 2048 x 4096 4.42-4.47 (12 x 16 tiles, DPP, edge modes, r6o-q)
+    (38.5, 4.90),   # 2192 x 4168 (the 4 x 2 8-GPU box at m = 7): 4.40-4.51 at 7-pass spans
     (41.0, 5.14),   # 1168 x 8192 (the 8 x 1 8-GPU box at m = 7, 7 full chunks): 4.67 at 7
     (72.0, 5.30),   # 2048 x 8192 5.25-5.34 / 4096^2 5.22-5.34 / 4144^2 5.37 (20 x 16)
 ]
